@@ -1,0 +1,821 @@
+// extern "C" boundary (include/fheregex.h): context, keys, ciphertext handles,
+// eager gate ops (the smart_* replacements), the batched has_match engine.
+#include <chrono>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "device.h"
+#include "fheregex.h"
+#include "keys.h"
+#include "lower.h"
+#include "regex.h"
+
+namespace fr {
+
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+Params params_from_c(const fr_params* c) {
+    Params p;
+    if (c) {
+        p.k = c->k;
+        p.N = c->N;
+        p.n = c->n;
+        p.ks_base_log = c->ks_base_log;
+        p.ks_level = c->ks_level;
+        p.pbs_base_log = c->pbs_base_log;
+        p.pbs_level = c->pbs_level;
+        p.lwe_sigma = c->lwe_sigma;
+        p.glwe_sigma = c->glwe_sigma;
+    }
+    validate_params(p);
+    return p;
+}
+void validate_params(const Params& p) {
+    if (p.k < 1 || p.k > 4 || p.N < 256 || p.N > 4096 || (p.N & (p.N - 1)) || p.n < 1 || p.n > 1024)
+        throw Error(FR_ERR_INVALID, "invalid params");
+    if (p.pbs_base_log != 23 || p.pbs_level != 1) throw Error(FR_ERR_INVALID, "only the 2^23 x 1 PBS gadget is supported");
+    if (p.ks_base_log < 1 || p.ks_base_log * p.ks_level > 63) throw Error(FR_ERR_INVALID, "invalid keyswitch gadget");
+}
+
+struct Block {
+    int slot = -1;     // -1: trivial block
+    uint8_t triv = 0;  // value of a trivial block (message, < 16)
+};
+struct HandleRec {
+    bool live = false;
+    bool is_bool = false;  // block 0 carries 0/1, blocks 1..3 trivial zero
+    Block b[4];
+};
+
+static double now_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+}  // namespace fr
+
+using namespace fr;
+
+struct fr_ctx {
+    Params p;
+    std::unique_ptr<Device> dev;
+    ClientKey ck;
+    bool has_ck = false;
+    std::vector<uint64_t> ksk, bsk;
+    bool has_sk = false;
+    std::vector<HandleRec> handles;
+    std::vector<uint32_t> free_handles;
+    int lowering = FR_LOWER_THRESHOLD;
+
+    Device& device() {
+        if (!dev) throw Error(FR_ERR_NO_DEVICE, "host-only context: no HIP device");
+        return *dev;
+    }
+    fr_ct new_handle(const HandleRec& r) {
+        uint32_t h;
+        if (!free_handles.empty()) {
+            h = free_handles.back();
+            free_handles.pop_back();
+            handles[h] = r;
+        } else {
+            h = (uint32_t)handles.size();
+            handles.push_back(r);
+        }
+        handles[h].live = true;
+        return h;
+    }
+    HandleRec& get(fr_ct h) {
+        if (h >= handles.size() || !handles[h].live) throw Error(FR_ERR_INVALID, "invalid ciphertext handle");
+        return handles[h];
+    }
+    void release(fr_ct h) {
+        HandleRec& r = get(h);
+        for (auto& b : r.b)
+            if (b.slot >= 0 && dev) dev->free_slot(b.slot);
+        r.live = false;
+        free_handles.push_back(h);
+    }
+};
+
+namespace fr {
+
+// ---------------------------------------------------------------- executor
+// Runs a PBS program whose negative sources refer to blocks of `inputs`
+// (input q = pos q: src = -(1 + q*4 + blk)).  Returns one slot per gate
+// (caller owns those slots).
+static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs,
+                                      fr_match_stats* st) {
+    Device& dev = ctx->device();
+    if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
+    std::vector<int> slot(gates.size(), -1);
+    std::vector<int> level(gates.size(), 0);
+    int maxl = 0;
+    for (size_t g = 0; g < gates.size(); ++g) {
+        int l = 0;
+        for (auto& in : gates[g].ins)
+            if (in.src >= 0) {
+                if ((size_t)in.src >= g) throw Error(FR_ERR_INVALID, "gate program is not topologically ordered");
+                l = std::max(l, level[in.src]);
+            }
+        level[g] = l + 1;
+        maxl = std::max(maxl, l + 1);
+    }
+    std::vector<std::vector<int>> by_level(maxl + 1);
+    for (size_t g = 0; g < gates.size(); ++g) by_level[level[g]].push_back((int)g);
+    for (size_t g = 0; g < gates.size(); ++g) slot[g] = dev.alloc_slot();
+    std::vector<DevGate> batch;
+    size_t maxw = 0;
+    for (int l = 1; l <= maxl; ++l) {
+        batch.clear();
+        for (int g : by_level[l]) {
+            const PGate& G = gates[g];
+            DevGate d;
+            std::memset(&d, 0, sizeof d);
+            int off = G.offset;
+            int nin = 0;
+            for (auto& in : G.ins) {
+                int s;
+                if (in.src >= 0) {
+                    s = slot[in.src];
+                } else {
+                    int cb = -in.src - 1;
+                    size_t q = (size_t)(cb / 4);
+                    if (q >= inputs.size()) throw Error(FR_ERR_INVALID, "gate input out of range");
+                    const HandleRec& h = ctx->get(inputs[q]);
+                    const Block& b = h.b[cb % 4];
+                    if (b.slot < 0) {
+                        off += in.w * (int)b.triv;
+                        continue;
+                    }
+                    s = b.slot;
+                }
+                if (nin >= 15) throw Error(FR_ERR_INVALID, "gate fan-in > 15");
+                d.in_slot[nin] = s;
+                d.in_w[nin] = in.w;
+                ++nin;
+            }
+            d.n_in = nin;
+            d.offset = off;
+            std::memcpy(d.lut, G.lut, 16);
+            d.out_slot = slot[g];
+            batch.push_back(d);
+        }
+        maxw = std::max(maxw, batch.size());
+        dev.run_level(batch.data(), batch.size());
+    }
+    if (st) {
+        st->pbs += gates.size();
+        st->levels += (uint64_t)maxl;
+        st->max_level_width = std::max<uint64_t>(st->max_level_width, maxw);
+    }
+    return slot;
+}
+
+// result handle of a program: boolean from a gate slot, maybe negated, or trivial
+static fr_ct finish_output(fr_ctx* ctx, const Program& prog, std::vector<int>& slots) {
+    HandleRec r;
+    r.is_bool = true;
+    if (prog.out_gate < 0) {
+        r.b[0].triv = (uint8_t)prog.out_const;
+    } else if (prog.out_w == 1 && prog.out_const == 0) {
+        r.b[0].slot = slots[prog.out_gate];
+        slots[prog.out_gate] = -1;
+    } else {
+        DevGate d;
+        std::memset(&d, 0, sizeof d);
+        d.n_in = 1;
+        d.in_slot[0] = slots[prog.out_gate];
+        d.in_w[0] = prog.out_w;
+        d.offset = prog.out_const;
+        d.out_slot = ctx->device().alloc_slot();
+        ctx->device().run_linear(d);
+        r.b[0].slot = d.out_slot;
+    }
+    for (int s : slots)
+        if (s >= 0) ctx->device().free_slot(s);
+    ctx->device().sync();
+    return ctx->new_handle(r);
+}
+
+static fr_ct run_program(fr_ctx* ctx, const Program& prog, const std::vector<fr_ct>& inputs, fr_match_stats* st) {
+    std::vector<int> slots = execute_gates(ctx, prog.gates, inputs, st);
+    return finish_output(ctx, prog, slots);
+}
+
+static int cblk(int pos, int blk) { return -(1 + pos * 4 + blk); }
+
+static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
+                        fr_match_stats* st) {
+    double t0 = now_ms();
+    ValueDag dag;
+    Recorded rec = record_has_match(dag, n, pattern ? pattern : "", lo, hi);
+    Program prog = lower(dag, rec.root, ctx->lowering);
+    double t1 = now_ms();
+    std::vector<fr_ct> inputs(content, content + n);
+    // validate referenced content handles
+    for (auto& g : prog.gates)
+        for (auto& in : g.ins)
+            if (in.src < 0) {
+                size_t q = (size_t)((-in.src - 1) / 4);
+                if (q >= n || content[q] == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
+                const HandleRec& h = ctx->get(content[q]);
+                if (h.is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
+            }
+    DeviceTimers before = ctx->device().timers();
+    fr_match_stats local{};
+    fr_ct out = run_program(ctx, prog, inputs, &local);
+    double t2 = now_ms();
+    if (st) {
+        std::memset(st, 0, sizeof *st);
+        st->ct_ops = rec.ct_ops;
+        st->cache_hits = rec.cache_hits;
+        st->n_branches = rec.n_branches;
+        st->pbs = local.pbs;
+        st->levels = local.levels;
+        st->max_level_width = local.max_level_width;
+        st->host_ms = t1 - t0;
+        st->device_ms = t2 - t1;
+        const DeviceTimers& after = ctx->device().timers();
+        st->br_kernel_ms = after.br_ms - before.br_ms;
+        st->ks_kernel_ms = after.ks_ms - before.ks_ms;
+        st->br_launches = after.br_launches - before.br_launches;
+        st->br_gates = after.br_gates - before.br_gates;
+    }
+    return out;
+}
+
+// eager op programs over input handles (pos 0 = a, pos 1 = b)
+static Program prog_cmp_const(int kind, uint8_t c) {
+    Program p;
+    PGate lo, hi;
+    lo.ins = {{cblk(0, 0), 1}, {cblk(0, 1), 4}};
+    hi.ins = {{cblk(0, 2), 1}, {cblk(0, 3), 4}};
+    PGate fin;
+    if (kind == 0) {  // eq: [lo == c_lo] + [hi == c_hi] == 2
+        lut_eq(lo.lut, c & 15);
+        lut_eq(hi.lut, c >> 4);
+        fin.ins = {{0, 1}, {1, 1}};
+        lut_eq(fin.lut, 2);
+    } else {  // gt / le over the signs: 3*s_hi + s_lo
+        lut_sign(lo.lut, c & 15);
+        lut_sign(hi.lut, c >> 4);
+        fin.ins = {{1, 3}, {0, 1}};
+        lut_gt3(fin.lut, kind == 2);
+    }
+    p.gates = {lo, hi, fin};
+    p.out_gate = 2;
+    p.out_w = 1;
+    compute_levels(p);
+    return p;
+}
+
+}  // namespace fr
+
+// =================================================================== C-ABI
+#define FR_TRY(...)                                   \
+    try {                                             \
+        __VA_ARGS__;                                       \
+        return FR_OK;                                 \
+    } catch (const fr::Error& e) {                    \
+        fr::set_last_error(e.what());                 \
+        return e.code;                                \
+    } catch (const std::bad_alloc&) {                 \
+        fr::set_last_error("out of memory");          \
+        return FR_ERR_OOM;                            \
+    } catch (const std::exception& e) {               \
+        fr::set_last_error(e.what());                 \
+        return FR_ERR_INVALID;                        \
+    } catch (...) {                                   \
+        fr::set_last_error("unknown error");          \
+        return FR_ERR_INVALID;                        \
+    }
+
+#define NEED(x)                                                               \
+    do {                                                                      \
+        if (!(x)) throw fr::Error(FR_ERR_INVALID, "invalid argument: " #x);   \
+    } while (0)
+
+extern "C" {
+
+const char* fr_last_error(void) { return fr::g_last_error.c_str(); }
+
+int fr_default_params(fr_params* out) {
+    FR_TRY({
+        NEED(out);
+        Params p;
+        std::memset(out, 0, sizeof *out);
+        out->k = p.k;
+        out->N = p.N;
+        out->n = p.n;
+        out->ks_base_log = p.ks_base_log;
+        out->ks_level = p.ks_level;
+        out->pbs_base_log = p.pbs_base_log;
+        out->pbs_level = p.pbs_level;
+        out->lwe_sigma = p.lwe_sigma;
+        out->glwe_sigma = p.glwe_sigma;
+    })
+}
+
+int fr_ctx_create(const fr_params* params, int device, fr_ctx** out) {
+    FR_TRY({
+        NEED(out);
+        *out = nullptr;
+        auto ctx = std::make_unique<fr_ctx>();
+        ctx->p = params_from_c(params);
+        if (device >= 0) ctx->dev = std::make_unique<Device>(ctx->p, device);
+        *out = ctx.release();
+    })
+}
+
+int fr_ctx_destroy(fr_ctx* ctx) {
+    FR_TRY({ delete ctx; })
+}
+
+int fr_set_lowering(fr_ctx* ctx, int32_t mode) {
+    FR_TRY({
+        NEED(ctx && (mode == FR_LOWER_FAITHFUL || mode == FR_LOWER_THRESHOLD));
+        ctx->lowering = mode;
+    })
+}
+
+int fr_set_profiling(fr_ctx* ctx, int32_t on) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->device().set_profiling(on != 0);
+    })
+}
+
+int fr_device_info(fr_ctx* ctx, char* buf, size_t len) {
+    FR_TRY({
+        NEED(ctx && buf && len);
+        std::string s = ctx->dev ? ctx->dev->info() : std::string("host-only");
+        std::snprintf(buf, len, "%s", s.c_str());
+    })
+}
+
+int fr_load_client_key(fr_ctx* ctx, const uint8_t* data, size_t len) {
+    FR_TRY({
+        NEED(ctx && data);
+        ClientKey ck = parse_client_key(data, len);
+        if ((size_t)ctx->p.k * ctx->p.N != ck.s_big.size() || (size_t)ctx->p.n != ck.s_small.size())
+            throw Error(FR_ERR_INVALID, "client key dimensions do not match the context params");
+        ctx->ck = std::move(ck);
+        ctx->has_ck = true;
+        ctx->has_sk = false;
+    })
+}
+
+int fr_gen_server_key(fr_ctx* ctx, uint64_t seed) {
+    FR_TRY({
+        NEED(ctx);
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        gen_ksk(ctx->p, ctx->ck, seed, ctx->ksk);
+        gen_bsk(ctx->p, ctx->ck, seed, ctx->bsk);
+        if (ctx->dev) ctx->dev->upload_keys(ctx->ksk, ctx->bsk);
+        ctx->has_sk = true;
+    })
+}
+
+int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len) {
+    FR_TRY({
+        NEED(ctx);
+        const Params& p = ctx->p;
+        if (ksk_len) *ksk_len = (size_t)p.big() * p.ks_level * (p.n + 1);
+        if (bsk_len) *bsk_len = (size_t)p.n * (p.k + 1) * (p.k + 1) * p.N;
+    })
+}
+
+int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len) {
+    FR_TRY({
+        NEED(ctx);
+        if (!ctx->has_sk) throw Error(FR_ERR_NO_KEY, "server key not generated");
+        if (ksk) {
+            NEED(ksk_len == ctx->ksk.size());
+            std::memcpy(ksk, ctx->ksk.data(), 8 * ksk_len);
+        }
+        if (bsk) {
+            NEED(bsk_len == ctx->bsk.size());
+            std::memcpy(bsk, ctx->bsk.data(), 8 * bsk_len);
+        }
+    })
+}
+
+int fr_encrypt_blocks(fr_ctx* ctx, const uint8_t* msgs, size_t count, uint64_t seed, uint64_t first_block,
+                      uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && (msgs || !count) && (out || !count));
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        for (size_t i = 0; i < count; ++i) NEED(msgs[i] < 16);
+        encrypt_blocks(ctx->p, ctx->ck, msgs, count, seed, first_block, out);
+    })
+}
+
+int fr_encrypt_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && (s || !len) && (out || !len));
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        std::vector<uint8_t> msgs(4 * len);
+        for (size_t i = 0; i < len; ++i) {
+            uint8_t c = (uint8_t)s[i];
+            if (c > 127) throw Error(FR_ERR_NON_ASCII, "content contains non-ascii characters");
+            for (int b = 0; b < 4; ++b) msgs[4 * i + b] = (c >> (2 * b)) & 3;  // ciphertext.rs:18-29
+        }
+        encrypt_blocks(ctx->p, ctx->ck, msgs.data(), msgs.size(), seed, 0, out);
+    })
+}
+
+int fr_decode_block(fr_ctx* ctx, const uint64_t* lwe, uint32_t* v) {
+    FR_TRY({
+        NEED(ctx && lwe && v);
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        *v = decode16(lwe_phase(ctx->p, ctx->ck, lwe));
+    })
+}
+
+int fr_decrypt_radix(fr_ctx* ctx, const uint64_t* blocks, uint64_t* value) {
+    FR_TRY({
+        NEED(ctx && blocks && value);
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        uint64_t v = 0;
+        for (int b = 0; b < 4; ++b) {
+            uint32_t d = decode16(lwe_phase(ctx->p, ctx->ck, blocks + (size_t)b * ctx->p.lwe_len()));
+            v += (uint64_t)(d % 4) << (2 * b);
+        }
+        *value = v & 0xFF;
+    })
+}
+
+int fr_upload_radix(fr_ctx* ctx, const uint64_t* blocks, size_t n, fr_ct* out) {
+    FR_TRY({
+        NEED(ctx && (blocks || !n) && (out || !n));
+        Device& dev = ctx->device();
+        const int L = ctx->p.lwe_len();
+        std::vector<int> slots(4 * n);
+        for (auto& s : slots) s = dev.alloc_slot();
+        dev.write_slots(slots.data(), slots.size(), blocks);
+        for (size_t i = 0; i < n; ++i) {
+            HandleRec r;
+            for (int b = 0; b < 4; ++b) r.b[b].slot = slots[4 * i + b];
+            out[i] = ctx->new_handle(r);
+        }
+        (void)L;
+    })
+}
+
+int fr_upload_bool(fr_ctx* ctx, const uint64_t* lwe, size_t n, fr_ct* out) {
+    FR_TRY({
+        NEED(ctx && (lwe || !n) && (out || !n));
+        Device& dev = ctx->device();
+        std::vector<int> slots(n);
+        for (auto& s : slots) s = dev.alloc_slot();
+        dev.write_slots(slots.data(), n, lwe);
+        for (size_t i = 0; i < n; ++i) {
+            HandleRec r;
+            r.is_bool = true;
+            r.b[0].slot = slots[i];
+            out[i] = ctx->new_handle(r);
+        }
+    })
+}
+
+int fr_download_radix(fr_ctx* ctx, fr_ct h, uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && out);
+        HandleRec& r = ctx->get(h);
+        const int L = ctx->p.lwe_len();
+        for (int b = 0; b < 4; ++b) {
+            uint64_t* o = out + (size_t)b * L;
+            if (r.b[b].slot >= 0) {
+                ctx->device().read_slot(r.b[b].slot, o);
+            } else {  // trivial block (shortint create_trivial): zero mask, body m * Delta
+                std::memset(o, 0, 8 * (size_t)L);
+                o[L - 1] = (uint64_t)r.b[b].triv << DELTA_LOG;
+            }
+        }
+    })
+}
+
+int fr_release(fr_ctx* ctx, fr_ct h) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->release(h);
+    })
+}
+
+int fr_trivial(fr_ctx* ctx, uint8_t value, fr_ct* out) {
+    FR_TRY({  // create_trivial_radix, ciphertext.rs:8-30
+        NEED(ctx && out);
+        HandleRec r;
+        for (int b = 0; b < 4; ++b) r.b[b].triv = (value >> (2 * b)) & 3;
+        *out = ctx->new_handle(r);
+    })
+}
+
+static int cmp_const_op(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out, int kind) {
+    FR_TRY({
+        NEED(ctx && out);
+        if (ctx->get(a).is_bool) throw Error(FR_ERR_INVALID, "comparison operand must be a radix character");
+        Program p = prog_cmp_const(kind, c);
+        *out = run_program(ctx, p, {a}, nullptr);
+    })
+}
+int fr_eq_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out) { return cmp_const_op(ctx, a, c, out, 0); }
+int fr_gt_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out) { return cmp_const_op(ctx, a, c, out, 1); }
+int fr_le_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out) { return cmp_const_op(ctx, a, c, out, 2); }
+
+static int bitop(fr_ctx* ctx, fr_ct a, fr_ct b, fr_ct* out, bool is_and) {
+    FR_TRY({
+        NEED(ctx && out);
+        const HandleRec& ha = ctx->get(a);
+        const HandleRec& hb = ctx->get(b);
+        if (ha.is_bool && hb.is_bool) {  // booleans: one bivariate PBS on block 0
+            Program p;
+            PGate g;
+            g.ins = {{cblk(0, 0), 1}, {cblk(1, 0), 1}};
+            if (is_and) lut_eq(g.lut, 2);
+            else lut_at_least(g.lut, 1);
+            p.gates = {g};
+            p.out_gate = 0;
+            p.out_w = 1;
+            compute_levels(p);
+            *out = run_program(ctx, p, {a, b}, nullptr);
+        } else {  // general radix: per block, LUT over 4*x + y
+            std::vector<PGate> gates(4);
+            for (int blk = 0; blk < 4; ++blk) {
+                gates[blk].ins = {{cblk(0, blk), 4}, {cblk(1, blk), 1}};
+                for (int v = 0; v < 16; ++v) gates[blk].lut[v] = (uint8_t)(is_and ? ((v >> 2) & (v & 3)) : ((v >> 2) | (v & 3)));
+            }
+            std::vector<int> slots = execute_gates(ctx, gates, {a, b}, nullptr);
+            ctx->device().sync();
+            HandleRec r;
+            for (int blk = 0; blk < 4; ++blk) r.b[blk].slot = slots[blk];
+            *out = ctx->new_handle(r);
+        }
+    })
+}
+int fr_and(fr_ctx* ctx, fr_ct a, fr_ct b, fr_ct* out) { return bitop(ctx, a, b, out, true); }
+int fr_or(fr_ctx* ctx, fr_ct a, fr_ct b, fr_ct* out) { return bitop(ctx, a, b, out, false); }
+
+int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out) {
+    FR_TRY({  // smart_bitxor(a, trivial 1), execution.rs:178-195
+        NEED(ctx && out);
+        const HandleRec ha = ctx->get(a);
+        if (ha.is_bool) {
+            HandleRec r;
+            r.is_bool = true;
+            if (ha.b[0].slot < 0) {
+                r.b[0].triv = ha.b[0].triv ^ 1;
+            } else {
+                DevGate d;
+                std::memset(&d, 0, sizeof d);
+                d.n_in = 1;
+                d.in_slot[0] = ha.b[0].slot;
+                d.in_w[0] = -1;
+                d.offset = 1;
+                d.out_slot = ctx->device().alloc_slot();
+                ctx->device().run_linear(d);
+                ctx->device().sync();
+                r.b[0].slot = d.out_slot;
+            }
+            *out = ctx->new_handle(r);
+        } else {  // general radix: block 0 through a LUT, blocks 1..3 copied
+            HandleRec r;
+            std::vector<PGate> gates(1);
+            gates[0].ins = {{cblk(0, 0), 1}};
+            for (int v = 0; v < 16; ++v) gates[0].lut[v] = (uint8_t)((v & 3) ^ 1);
+            std::vector<int> slots = execute_gates(ctx, gates, {a}, nullptr);
+            r.b[0].slot = slots[0];
+            for (int blk = 1; blk < 4; ++blk) {
+                if (ha.b[blk].slot < 0) {
+                    r.b[blk] = ha.b[blk];
+                    continue;
+                }
+                DevGate d;
+                std::memset(&d, 0, sizeof d);
+                d.n_in = 1;
+                d.in_slot[0] = ha.b[blk].slot;
+                d.in_w[0] = 1;
+                d.out_slot = ctx->device().alloc_slot();
+                ctx->device().run_linear(d);
+                r.b[blk].slot = d.out_slot;
+            }
+            ctx->device().sync();
+            *out = ctx->new_handle(r);
+        }
+    })
+}
+
+int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out) {
+    FR_TRY({
+        NEED(ctx && out && (in || !n));
+        std::vector<fr_ct> inputs;
+        int triv_or = 0;
+        for (size_t i = 0; i < n; ++i) {
+            const HandleRec& h = ctx->get(in[i]);
+            if (!h.is_bool) throw Error(FR_ERR_INVALID, "fr_or_many: inputs must be booleans");
+            if (h.b[0].slot < 0) triv_or |= h.b[0].triv & 1;
+            else inputs.push_back(in[i]);
+        }
+        HandleRec r;
+        r.is_bool = true;
+        if (triv_or || inputs.empty()) {
+            r.b[0].triv = (uint8_t)triv_or;
+            *out = ctx->new_handle(r);
+            return FR_OK;
+        }
+        if (inputs.size() == 1) {  // copy
+            DevGate d;
+            std::memset(&d, 0, sizeof d);
+            d.n_in = 1;
+            d.in_slot[0] = ctx->get(inputs[0]).b[0].slot;
+            d.in_w[0] = 1;
+            d.out_slot = ctx->device().alloc_slot();
+            ctx->device().run_linear(d);
+            ctx->device().sync();
+            r.b[0].slot = d.out_slot;
+            *out = ctx->new_handle(r);
+            return FR_OK;
+        }
+        // balanced tree of <= 15-input threshold ORs
+        Program p;
+        std::vector<int> cur;  // sources: negative = input q, else gate
+        for (size_t q = 0; q < inputs.size(); ++q) cur.push_back(cblk((int)q, 0));
+        while (cur.size() > 1) {
+            std::vector<int> next;
+            size_t m = cur.size(), chunks = (m + MAX_FANIN - 1) / MAX_FANIN, start = 0;
+            for (size_t c = 0; c < chunks; ++c) {
+                size_t len = m / chunks + (c < m % chunks ? 1 : 0);
+                if (len == 1) {
+                    next.push_back(cur[start]);
+                } else {
+                    PGate g;
+                    for (size_t t = 0; t < len; ++t) g.ins.push_back({cur[start + t], 1});
+                    lut_at_least(g.lut, 1);
+                    p.gates.push_back(g);
+                    next.push_back((int)p.gates.size() - 1);
+                }
+                start += len;
+            }
+            cur = next;
+        }
+        p.out_gate = cur[0];
+        p.out_w = 1;
+        compute_levels(p);
+        *out = run_program(ctx, p, inputs, nullptr);
+    })
+}
+
+int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n) {
+    FR_TRY({
+        NEED(ctx && (gates || !n));
+        std::vector<fr_ct> inputs;
+        std::vector<std::pair<fr_ct, int>> seen;
+        auto input_index = [&](fr_ct h) -> int {
+            for (size_t i = 0; i < inputs.size(); ++i)
+                if (inputs[i] == h) return (int)i;
+            ctx->get(h);
+            inputs.push_back(h);
+            return (int)inputs.size() - 1;
+        };
+        std::vector<PGate> pg(n);
+        for (size_t j = 0; j < n; ++j) {
+            const fr_gate& g = gates[j];
+            NEED(g.n_in >= 0 && g.n_in <= 15);
+            pg[j].offset = g.offset;
+            std::memcpy(pg[j].lut, g.lut, 16);
+            for (int q = 0; q < g.n_in; ++q) {
+                if (g.in[q] & 0x80000000u) {
+                    uint32_t src = g.in[q] & 0x7FFFFFFFu;
+                    NEED(src < j);
+                    pg[j].ins.push_back({(int)src, g.in_w[q]});
+                } else {
+                    NEED(g.in_block[q] >= 0 && g.in_block[q] < 4);
+                    pg[j].ins.push_back({cblk(input_index(g.in[q]), g.in_block[q]), g.in_w[q]});
+                }
+            }
+        }
+        std::vector<int> slots = execute_gates(ctx, pg, inputs, nullptr);
+        ctx->device().sync();
+        for (size_t j = 0; j < n; ++j) {
+            HandleRec r;
+            r.is_bool = true;
+            r.b[0].slot = slots[j];
+            gates[j].out = ctx->new_handle(r);
+        }
+    })
+}
+
+int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, fr_ct* out, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && out && pattern && (content || !n));
+        *out = match_impl(ctx, content, n, pattern, 0, n, st);
+    })
+}
+
+int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
+                       fr_ct* out, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && out && pattern && (content || !n) && lo <= hi);
+        *out = match_impl(ctx, content, n, pattern, lo, hi, st);
+    })
+}
+
+int fr_parse(const char* pattern, char* buf, size_t len) {
+    FR_TRY({
+        NEED(pattern && buf && len);
+        std::string s = to_string(*parse(pattern));
+        if (s.size() + 1 > len) throw Error(FR_ERR_INVALID, "buffer too small");
+        std::memcpy(buf, s.c_str(), s.size() + 1);
+    })
+}
+
+int fr_plain_match(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                   fr_plain_result* out) {
+    FR_TRY({
+        NEED((content || !len) && pattern && out && lo <= hi);
+        ValueDag dag;
+        Recorded rec = record_has_match(dag, len, pattern, lo, hi);
+        std::vector<int16_t> memo;
+        std::memset(out, 0, sizeof *out);
+        out->ct_ops = rec.ct_ops;
+        out->cache_hits = rec.cache_hits;
+        out->n_branches = rec.n_branches;
+        out->result_recorded = dag.eval(rec.root, (const uint8_t*)content, memo);
+        Program prog = lower(dag, rec.root, lowering);
+        out->pbs = prog.gates.size();
+        out->levels = (uint64_t)prog.levels;
+        out->max_level_width = prog.max_width;
+        out->result_lowered = eval_program(prog, (const uint8_t*)content, len);
+    })
+}
+
+int fr_dev_keyswitch(fr_ctx* ctx, const uint64_t* in, size_t count, uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && in && out);
+        ctx->device().keyswitch_host(in, count, out);
+    })
+}
+int fr_dev_blind_rotate(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, size_t count, uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && in && luts && out);
+        ctx->device().blind_rotate_host(in, luts, count, out);
+    })
+}
+int fr_dev_ring_mul(fr_ctx* ctx, const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && a && b && out);
+        ctx->device().ring_mul_host(a, b, count, out);
+    })
+}
+int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, double* br_ms, double* total_ms) {
+    FR_TRY({
+        NEED(ctx && in && count && iters > 0 && br_ms && total_ms);
+        Device& dev = ctx->device();
+        if (!ctx->has_sk) throw Error(FR_ERR_NO_KEY, "server key not generated");
+        std::vector<DevGate> gates(count);
+        std::vector<int> outs(count);
+        for (size_t i = 0; i < count; ++i) {
+            const HandleRec& h = ctx->get(in[i]);
+            DevGate& d = gates[i];
+            std::memset(&d, 0, sizeof d);
+            int nin = 0, off = 0;
+            // pack x0 + 4*x1 of a radix char (or a boolean's block 0): an eq-nibble PBS
+            const int w[2] = {1, 4};
+            for (int b = 0; b < (h.is_bool ? 1 : 2); ++b) {
+                if (h.b[b].slot < 0) {
+                    off += w[b] * h.b[b].triv;
+                    continue;
+                }
+                d.in_slot[nin] = h.b[b].slot;
+                d.in_w[nin] = w[b];
+                ++nin;
+            }
+            d.n_in = nin;
+            d.offset = off;
+            lut_eq(d.lut, 1);
+            outs[i] = dev.alloc_slot();
+            d.out_slot = outs[i];
+        }
+        dev.bench_pbs(gates, iters, br_ms, total_ms);
+        for (int s : outs) dev.free_slot(s);
+    })
+}
+
+uint64_t fr_debug_scalar(int32_t op, uint64_t x, uint64_t y) {
+    switch (op) {
+        case 0: return gl_mul(x, y);
+        case 1: return pbs_decompose(x);
+        case 2: return zp_to_torus(x);
+        case 3: return mod_switch(x, (int)y);
+        case 4: {
+            int32_t d[5];
+            ks_decompose<3, 5>(x, d);
+            return (uint64_t)(int64_t)d[y % 5];
+        }
+        default: return 0;
+    }
+}
+
+}  // extern "C"

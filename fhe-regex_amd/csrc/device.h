@@ -1,0 +1,92 @@
+// Device executor interface (HIP, gfx950).  Kernels live in device.hip.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "common.h"
+
+namespace fr {
+
+// One programmable bootstrap as the device sees it:
+//   out_slot <- PBS_lut( offset*2^59 + sum_q w_q * arena[in_slot_q] )
+struct DevGate {
+    int32_t n_in;
+    int32_t offset;
+    int32_t in_slot[15];
+    int32_t in_w[15];
+    uint8_t lut[16];
+    int32_t out_slot;
+    int32_t _pad;
+};
+static_assert(sizeof(DevGate) == 136 + 16, "DevGate layout");
+
+struct DeviceTimers {
+    double br_ms = 0, ks_ms = 0;
+    uint64_t br_launches = 0, br_gates = 0;
+};
+
+class Device {
+  public:
+    Device(const Params& p, int device);
+    ~Device();
+    Device(const Device&) = delete;
+    Device& operator=(const Device&) = delete;
+
+    const Params& params() const { return p_; }
+    int device() const { return dev_; }
+
+    // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod P [i][r][c][coef]
+    void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
+    bool has_keys() const { return d_ksk_ && d_bsk_; }
+
+    // arena of big-LWE slots
+    int alloc_slot();
+    void free_slot(int s);
+    void write_slots(const int* slots, size_t n, const uint64_t* host /* n * lwe_len */);
+    void read_slot(int slot, uint64_t* host /* lwe_len */);
+    void zero_slot(int slot);
+
+    // run one dependency level of gates (all independent), async on the stream
+    void run_level(const DevGate* gates, size_t n);
+    // linear combination without bootstrap (NOT of a boolean): out = offset*2^59 + sum w*in
+    void run_linear(const DevGate& g);
+    void sync();
+
+    void set_profiling(bool on) { profiling_ = on; }
+    DeviceTimers& timers() { return timers_; }
+
+    // single-stage entry points for parity tests
+    void keyswitch_host(const uint64_t* in, size_t count, uint64_t* out);
+    void blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_t count, uint64_t* out);
+    void ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out);
+    // repeated full-PBS batches on resident inputs (bench / roofline)
+    void bench_pbs(const std::vector<DevGate>& gates, int iters, double* br_ms, double* total_ms);
+
+    std::string info() const;
+
+  private:
+    void ensure_arena(size_t slots);
+    void ensure_batch(size_t n);
+    void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks);
+    void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n);
+
+    Params p_;
+    int dev_;
+    void* stream_ = nullptr;  // hipStream_t
+    uint64_t* d_ksk_ = nullptr;
+    uint64_t* d_bsk_ = nullptr;  // NTT domain, scaled by 1/N
+    uint64_t* d_tw_ = nullptr;   // zeta[N], izeta[N]
+    uint64_t* d_arena_ = nullptr;
+    size_t arena_cap_ = 0;
+    std::vector<int> free_slots_;
+    size_t next_slot_ = 0;
+    DevGate* d_gates_ = nullptr;
+    DevGate* h_gates_ = nullptr;  // pinned staging
+    uint64_t* d_ks_ = nullptr;
+    size_t batch_cap_ = 0;
+    bool profiling_ = false;
+    DeviceTimers timers_;
+    void* ev_[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+
+}  // namespace fr

@@ -1,0 +1,752 @@
+// HIP kernels for the TFHE gate bootstrap on MI355X (gfx950, CDNA4).
+//
+//   k_lincomb_keyswitch : lincomb of input LWEs (mod 2^64) fused with the
+//                         LWE keyswitch kN -> n (signed base 2^3, 5 levels)
+//   k_blind_rotate<N,K> : modulus switch, LUT accumulator, n CMUX steps
+//                         (rotate -> gadget decompose -> forward NTT -> MAC with
+//                         the NTT-domain GGSW -> inverse NTT -> accumulate),
+//                         sample extract, Z_p -> 2^64 conversion.
+//                         One workgroup of (K+1)*N/16 threads per bootstrap:
+//                         each polynomial is owned by N/16 lanes holding 16
+//                         coefficients in registers; the 11 NTT stages run as
+//                         3 register-resident phases (4+4+3 stages) joined by
+//                         two LDS exchanges.
+//   k_bsk_to_ntt<N,K>   : one-time forward NTT of the bootstrapping key.
+//
+// Arithmetic: Goldilocks prime P = 2^64 - 2^32 + 1 (common.h), 64x64->128 via
+// four v_mad_u64_u32, reduction with shifts/adds only.  The NTT is the
+// merged-psi negacyclic Cooley-Tukey (forward) / Gentleman-Sande (inverse)
+// transform: zeta[k] = psi^brv(k); outputs in bit-reversed slot order.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <sstream>
+
+#include "device.h"
+#include "keys.h"
+
+namespace fr {
+
+#define HIP_CHECK(x)                                                                         \
+    do {                                                                                     \
+        hipError_t _e = (x);                                                                 \
+        if (_e != hipSuccess)                                                                \
+            throw Error(FR_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(_e) +     \
+                                        " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+// ------------------------------------------------------------------ geometry
+template <int N>
+struct Geom {
+    static constexpr int LOG = (N == 2048) ? 11 : (N == 1024) ? 10 : (N == 512) ? 9 : 0;
+    static_assert(LOG >= 9, "N must be 512, 1024 or 2048");
+    static constexpr int T = N / 16;   // lanes per polynomial
+    static constexpr int R = N / 256;  // phase-2 lane stride
+    static constexpr int NP = N + N / 16;  // padded LDS row (u64)
+    __device__ static __forceinline__ int pad(int i) { return i + (i >> 4); }
+    __device__ static __forceinline__ int idx1(int tl, int m) { return tl + T * m; }
+    __device__ static __forceinline__ int idx2(int tl, int m) { return (tl / R) * T + (tl % R) + R * m; }
+    __device__ static __forceinline__ int idx3(int tl, int m) { return 16 * tl + m; }
+};
+
+__device__ __forceinline__ void ct_bf(uint64_t& x, uint64_t& y, uint64_t z) {
+    uint64_t t = gl_mul(z, y);
+    y = gl_sub(x, t);
+    x = gl_add(x, t);
+}
+__device__ __forceinline__ void gs_bf(uint64_t& x, uint64_t& y, uint64_t z) {
+    uint64_t u = x, v = y;
+    x = gl_add(u, v);
+    y = gl_mul(gl_sub(u, v), z);
+}
+
+// ----- forward phases (stage s: distance N >> (s+1); zeta index (1<<s) + (j >> (LOG-s)))
+template <int N>
+__device__ __forceinline__ void fwd_phase1(uint64_t (&x)[16], const uint64_t* zt) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int d = 8 >> q;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = zt[(1 << q) + (m >> (4 - q))];
+            ct_bf(x[m], x[m + d], z);
+        }
+    }
+}
+template <int N>
+__device__ __forceinline__ void fwd_phase2(uint64_t (&x)[16], const uint64_t* zt, int tl) {
+    using G = Geom<N>;
+    const int c = tl / G::R;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int s = 4 + q, d = 8 >> q;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = zt[(1 << s) + (c << q) + (m >> (4 - q))];
+            ct_bf(x[m], x[m + d], z);
+        }
+    }
+}
+template <int N>
+__device__ __forceinline__ void fwd_phase3(uint64_t (&x)[16], const uint64_t* zt, int tl) {
+    using G = Geom<N>;
+#pragma unroll
+    for (int s = 8; s < G::LOG; ++s) {
+        const int d = N >> (s + 1);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = zt[(1 << s) + ((16 * tl + m) >> (G::LOG - s))];
+            ct_bf(x[m], x[m + d], z);
+        }
+    }
+}
+// ----- inverse phases (reverse order, GS butterflies with izeta)
+template <int N>
+__device__ __forceinline__ void inv_phase3(uint64_t (&x)[16], const uint64_t* izt, int tl) {
+    using G = Geom<N>;
+#pragma unroll
+    for (int s = G::LOG - 1; s >= 8; --s) {
+        const int d = N >> (s + 1);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = izt[(1 << s) + ((16 * tl + m) >> (G::LOG - s))];
+            gs_bf(x[m], x[m + d], z);
+        }
+    }
+}
+template <int N>
+__device__ __forceinline__ void inv_phase2(uint64_t (&x)[16], const uint64_t* izt, int tl) {
+    using G = Geom<N>;
+    const int c = tl / G::R;
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+        const int s = 4 + q, d = 8 >> q;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = izt[(1 << s) + (c << q) + (m >> (4 - q))];
+            gs_bf(x[m], x[m + d], z);
+        }
+    }
+}
+template <int N>
+__device__ __forceinline__ void inv_phase1(uint64_t (&x)[16], const uint64_t* izt) {
+#pragma unroll
+    for (int q = 3; q >= 0; --q) {
+        const int d = 8 >> q;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            if (m & d) continue;
+            const uint64_t z = izt[(1 << q) + (m >> (4 - q))];
+            gs_bf(x[m], x[m + d], z);
+        }
+    }
+}
+
+// LDS exchange between lane layouts (row = this lane's polynomial)
+template <int N, int FROM, int TO>
+__device__ __forceinline__ void exchange(uint64_t (&x)[16], uint64_t* row, int tl) {
+    using G = Geom<N>;
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        int i = FROM == 1 ? G::idx1(tl, m) : FROM == 2 ? G::idx2(tl, m) : G::idx3(tl, m);
+        row[G::pad(i)] = x[m];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        int i = TO == 1 ? G::idx1(tl, m) : TO == 2 ? G::idx2(tl, m) : G::idx3(tl, m);
+        x[m] = row[G::pad(i)];
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void forward_ntt(uint64_t (&x)[16], uint64_t* row, const uint64_t* zt, int tl) {
+    fwd_phase1<N>(x, zt);
+    exchange<N, 1, 2>(x, row, tl);
+    fwd_phase2<N>(x, zt, tl);
+    exchange<N, 2, 3>(x, row, tl);
+    fwd_phase3<N>(x, zt, tl);
+}
+template <int N>
+__device__ __forceinline__ void inverse_ntt(uint64_t (&x)[16], uint64_t* row, const uint64_t* izt, int tl) {
+    inv_phase3<N>(x, izt, tl);
+    exchange<N, 3, 2>(x, row, tl);
+    inv_phase2<N>(x, izt, tl);
+    exchange<N, 2, 1>(x, row, tl);
+    inv_phase1<N>(x, izt);
+}
+
+// ------------------------------------------------------------ blind rotation
+template <int N, int K>
+constexpr size_t br_smem_bytes() {
+    return sizeof(uint64_t) * ((size_t)(K + 1) * Geom<N>::NP + 2 * (size_t)N) + 16 + 2 * 1024;
+}
+
+template <int N, int K>
+__global__ void __launch_bounds__((K + 1) * (N / 16))
+k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
+               const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ tw, uint64_t* __restrict__ arena,
+               int slot_stride) {
+    using G = Geom<N>;
+    constexpr int NT = (K + 1) * G::T;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* xbuf = smem;                       // (K+1) rows of NP
+    uint64_t* zt = xbuf + (K + 1) * G::NP;       // N
+    uint64_t* izt = zt + N;                      // N
+    uint8_t* lut = (uint8_t*)(izt + N);          // 16
+    uint16_t* abar = (uint16_t*)(lut + 16);      // n (<= 1024)
+
+    const int tid = threadIdx.x;
+    const int P = tid / G::T, tl = tid % G::T;
+    const int g = blockIdx.x;
+    const uint64_t* in = ks + (size_t)g * ks_stride;
+
+    for (int i = tid; i < N; i += NT) {
+        zt[i] = tw[i];
+        izt[i] = tw[N + i];
+    }
+    if (tid < 16) lut[tid] = gates[g].lut[tid];
+    for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
+    const uint32_t bbar = mod_switch(in[n], G::LOG + 1);
+    __syncthreads();
+
+    uint64_t* row = xbuf + P * G::NP;
+    uint64_t acc[16];
+    {
+        constexpr int box = N / 16, half = box / 2;
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            acc[m] = 0;
+            if (P == K) {
+                int s = (G::idx1(tl, m) + (int)bbar) & (2 * N - 1);
+                int sp = s < N ? s : s - N;
+                int mm = (sp + half) / box;
+                uint64_t v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
+                acc[m] = s < N ? v : gl_neg(v);
+            }
+        }
+    }
+
+    const size_t ggsw = (size_t)(K + 1) * (K + 1) * N;
+    for (int i = 0; i < n; ++i) {
+        const int a = abar[i];
+        if (a == 0) continue;  // X^0*acc - acc = 0: exact no-op (uniform branch)
+        // 1. rotate (X^a - 1) * acc and decompose
+        uint64_t x[16];
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) row[G::pad(G::idx1(tl, m))] = acc[m];
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            int s = (G::idx1(tl, m) - a) & (2 * N - 1);
+            uint64_t v = s < N ? row[G::pad(s)] : gl_neg(row[G::pad(s - N)]);
+            x[m] = pbs_decompose(gl_sub(v, acc[m]));
+        }
+        // 2. forward NTT of this lane group's digit polynomial
+        forward_ntt<N>(x, row, zt, tl);
+        // 3. external product MAC: out_P = sum_r D_r * GGSW_i[r][P]
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < 16; ++m) row[G::pad(G::idx3(tl, m))] = x[m];
+        __syncthreads();
+        const uint64_t* gi = bsk + (size_t)i * ggsw;
+        uint64_t y[16];
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+            const int pos = G::pad(G::idx3(tl, m));
+            uint64_t sacc = 0;
+#pragma unroll
+            for (int r = 0; r <= K; ++r) {
+                const uint64_t d = (r == P) ? x[m] : xbuf[r * G::NP + pos];
+                const uint64_t gv = gi[((size_t)(r * (K + 1) + P)) * N + m * G::T + tl];
+                sacc = gl_add(sacc, gl_mul(d, gv));
+            }
+            y[m] = sacc;
+        }
+        // 4. inverse NTT and accumulate
+        inverse_ntt<N>(y, row, izt, tl);
+#pragma unroll
+        for (int m = 0; m < 16; ++m) acc[m] = gl_add(acc[m], y[m]);
+    }
+
+    // sample extract (coefficient 0) under the flattened key, then Z_p -> 2^64
+    uint64_t* out = arena + (size_t)gates[g].out_slot * slot_stride;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int j = G::idx1(tl, m);
+        if (P < K) {
+            const int t = j == 0 ? 0 : N - j;
+            const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
+            out[P * N + t] = zp_to_torus(v);
+        } else if (j == 0) {
+            out[K * N] = zp_to_torus(acc[m]);
+        }
+    }
+}
+
+// ------------------------------------------------------ BSK -> NTT domain
+template <int N, int K>
+__global__ void __launch_bounds__((K + 1) * (N / 16))
+k_bsk_to_ntt(const uint64_t* __restrict__ coef, const uint64_t* __restrict__ tw, uint64_t n_inv,
+             uint64_t* __restrict__ out) {
+    using G = Geom<N>;
+    constexpr int NT = (K + 1) * G::T;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* xbuf = smem;
+    uint64_t* zt = xbuf + (K + 1) * G::NP;
+    const int tid = threadIdx.x, P = tid / G::T, tl = tid % G::T;
+    for (int i = tid; i < N; i += NT) zt[i] = tw[i];
+    __syncthreads();
+    const size_t poly = ((size_t)blockIdx.x * (K + 1) + P) * N;  // blockIdx.x = i*(K+1) + r
+    uint64_t x[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) x[m] = coef[poly + G::idx1(tl, m)];
+    forward_ntt<N>(x, xbuf + P * G::NP, zt, tl);
+#pragma unroll
+    for (int m = 0; m < 16; ++m) out[poly + m * G::T + tl] = gl_mul(x[m], n_inv);
+}
+
+// ------------------------------------------------ ring product (parity test)
+template <int N>
+__global__ void __launch_bounds__(2 * (N / 16))
+k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const uint64_t* __restrict__ tw,
+           uint64_t n_inv, uint64_t* __restrict__ out) {
+    using G = Geom<N>;
+    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
+    uint64_t* xbuf = smem;
+    uint64_t* zt = xbuf + 2 * G::NP;
+    uint64_t* izt = zt + N;
+    const int tid = threadIdx.x, P = tid / G::T, tl = tid % G::T;
+    for (int i = tid; i < N; i += 2 * G::T) {
+        zt[i] = tw[i];
+        izt[i] = tw[N + i];
+    }
+    __syncthreads();
+    const uint64_t* src = (P == 0 ? a : b) + (size_t)blockIdx.x * N;
+    uint64_t x[16];
+#pragma unroll
+    for (int m = 0; m < 16; ++m) x[m] = src[G::idx1(tl, m)];
+    uint64_t* row = xbuf + P * G::NP;
+    forward_ntt<N>(x, row, zt, tl);
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) row[G::pad(G::idx3(tl, m))] = x[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+        const int pos = G::pad(G::idx3(tl, m));
+        x[m] = gl_mul(gl_mul(xbuf[pos], xbuf[G::NP + pos]), n_inv);
+    }
+    inverse_ntt<N>(x, row, izt, tl);
+    if (P == 0) {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) out[(size_t)blockIdx.x * N + G::idx1(tl, m)] = x[m];
+    }
+}
+
+// ------------------------------------------------- lincomb + keyswitch
+// Tile: 32 gates x 64 output columns per 256-thread workgroup.  Each wave owns
+// 8 gates; each lane one column.  Digits of the lincomb'd mask coefficients
+// are staged in LDS per chunk of 32 coefficients; KSK rows are read once per
+// tile, coalesced (64 consecutive u64 per wave).
+constexpr int KS_BT = 32, KS_CT = 64, KS_CH = 32;
+
+template <int KSB, int KSL>
+__global__ void __launch_bounds__(256)
+k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
+                    const uint64_t* __restrict__ ksk, int n, int big, uint64_t* __restrict__ out, int out_stride) {
+    __shared__ int8_t dig[KS_BT][KS_CH][KSL];
+    __shared__ DevGate sg[KS_BT];
+    const int tid = threadIdx.x;
+    const int col = blockIdx.y * KS_CT + (tid & 63);
+    const int rg = tid >> 6;
+    const int b0 = blockIdx.x * KS_BT;
+    for (int e = tid; e < KS_BT; e += 256) {
+        if (b0 + e < B) sg[e] = gates[b0 + e];
+        else sg[e].n_in = 0, sg[e].offset = 0;
+    }
+    uint64_t acc[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) acc[r] = 0;
+    for (int i0 = 0; i0 < big; i0 += KS_CH) {
+        __syncthreads();
+        for (int e = tid; e < KS_BT * KS_CH; e += 256) {
+            const int row = e / KS_CH, ii = e % KS_CH;
+            uint64_t v = 0;
+            if (i0 + ii < big) {
+                const DevGate& gg = sg[row];
+                for (int q = 0; q < gg.n_in; ++q)
+                    v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i0 + ii];
+            }
+            int32_t d[KSL];
+            ks_decompose<KSB, KSL>(v, d);
+#pragma unroll
+            for (int j = 0; j < KSL; ++j) dig[row][ii][j] = (int8_t)d[j];
+        }
+        __syncthreads();
+        if (col <= n) {
+            const int lim = big - i0 < KS_CH ? big - i0 : KS_CH;
+            for (int ii = 0; ii < lim; ++ii) {
+#pragma unroll
+                for (int j = 0; j < KSL; ++j) {
+                    const uint64_t kv = ksk[((size_t)(i0 + ii) * KSL + j) * (n + 1) + col];
+#pragma unroll
+                    for (int r = 0; r < 8; ++r) {
+                        const int64_t d = dig[rg * 8 + r][ii][j];
+                        acc[r] -= (uint64_t)d * kv;
+                    }
+                }
+            }
+        }
+    }
+    if (col <= n) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            const int row = rg * 8 + r, b = b0 + row;
+            if (b >= B) continue;
+            uint64_t v = acc[r];
+            if (col == n) {
+                const DevGate& gg = sg[row];
+                uint64_t body = (uint64_t)(int64_t)gg.offset << DELTA_LOG;
+                for (int q = 0; q < gg.n_in; ++q)
+                    body += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + big];
+                v += body;
+            }
+            out[(size_t)b * out_stride + col] = v;
+        }
+    }
+}
+
+// linear combination into a slot (no bootstrap): NOT of a boolean
+__global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, uint64_t* __restrict__ arena,
+                                                int slot_stride, int len) {
+    const DevGate gg = *g;
+    uint64_t* out = arena + (size_t)gg.out_slot * slot_stride;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < len; t += gridDim.x * 256) {
+        uint64_t v = (t == len - 1) ? ((uint64_t)(int64_t)gg.offset << DELTA_LOG) : 0;
+        for (int q = 0; q < gg.n_in; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + t];
+        out[t] = v;
+    }
+}
+
+// ================================================================== host side
+#define STREAM ((hipStream_t)stream_)
+
+template <int N, int K>
+static void set_smem_attr() {
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate<N, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)br_smem_bytes<N, K>()));
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_bsk_to_ntt<N, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)br_smem_bytes<N, K>()));
+}
+
+static bool supported(const Params& p) {
+    return (p.N == 2048 && p.k == 1) || (p.N == 1024 && p.k == 2) || (p.N == 1024 && p.k == 1);
+}
+
+Device::Device(const Params& p, int device) : p_(p), dev_(device) {
+    if (!supported(p)) throw Error(FR_ERR_INVALID, "device: unsupported (k, N)");
+    if (p.ks_base_log != 3 || p.ks_level != 5 || p.pbs_base_log != 23 || p.pbs_level != 1)
+        throw Error(FR_ERR_INVALID, "device: only KS 2^3x5 and PBS 2^23x1 are compiled");
+    if (p.n > 1024) throw Error(FR_ERR_INVALID, "device: n > 1024");
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0)
+        throw Error(FR_ERR_NO_DEVICE, "no usable HIP device " + std::to_string(device));
+    HIP_CHECK(hipSetDevice(device));
+    hipStream_t s;
+    HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    stream_ = s;
+    for (auto& e : ev_) {
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreate(&ev));
+        e = ev;
+    }
+    if (p.N == 2048 && p.k == 1) set_smem_attr<2048, 1>();
+    if (p.N == 1024 && p.k == 2) set_smem_attr<1024, 2>();
+    if (p.N == 1024 && p.k == 1) set_smem_attr<1024, 1>();
+    // twiddles
+    NttTables T(p.N);
+    std::vector<uint64_t> tw(2 * (size_t)p.N);
+    for (int i = 0; i < p.N; ++i) {
+        tw[i] = T.zeta[i];
+        tw[p.N + i] = T.izeta[i];
+    }
+    HIP_CHECK(hipMalloc(&d_tw_, 8 * tw.size()));
+    HIP_CHECK(hipMemcpy(d_tw_, tw.data(), 8 * tw.size(), hipMemcpyHostToDevice));
+    ensure_arena(1024);
+    ensure_batch(1024);
+}
+
+Device::~Device() {
+    (void)hipSetDevice(dev_);
+    if (stream_) (void)hipStreamSynchronize(STREAM);
+    (void)hipFree(d_ksk_);
+    (void)hipFree(d_bsk_);
+    (void)hipFree(d_tw_);
+    (void)hipFree(d_arena_);
+    (void)hipFree(d_gates_);
+    (void)hipFree(d_ks_);
+    if (h_gates_) (void)hipHostFree(h_gates_);
+    for (auto e : ev_)
+        if (e) (void)hipEventDestroy((hipEvent_t)e);
+    if (stream_) (void)hipStreamDestroy(STREAM);
+}
+
+std::string Device::info() const {
+    hipDeviceProp_t prop;
+    (void)hipGetDeviceProperties(&prop, dev_);
+    std::ostringstream o;
+    o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount;
+    return o.str();
+}
+
+void Device::ensure_arena(size_t slots) {
+    if (slots <= arena_cap_) return;
+    size_t cap = arena_cap_ ? arena_cap_ : 1024;
+    while (cap < slots) cap *= 2;
+    uint64_t* nb = nullptr;
+    HIP_CHECK(hipMalloc(&nb, (size_t)8 * p_.slot_stride() * cap));
+    if (d_arena_) {
+        HIP_CHECK(hipMemcpyAsync(nb, d_arena_, (size_t)8 * p_.slot_stride() * arena_cap_, hipMemcpyDeviceToDevice, STREAM));
+        HIP_CHECK(hipStreamSynchronize(STREAM));
+        HIP_CHECK(hipFree(d_arena_));
+    }
+    d_arena_ = nb;
+    arena_cap_ = cap;
+}
+
+void Device::ensure_batch(size_t n) {
+    if (n <= batch_cap_) return;
+    size_t cap = batch_cap_ ? batch_cap_ : 1024;
+    while (cap < n) cap *= 2;
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    (void)hipFree(d_gates_);
+    (void)hipFree(d_ks_);
+    if (h_gates_) (void)hipHostFree(h_gates_);
+    HIP_CHECK(hipMalloc(&d_gates_, sizeof(DevGate) * cap));
+    HIP_CHECK(hipHostMalloc(&h_gates_, sizeof(DevGate) * cap));
+    HIP_CHECK(hipMalloc(&d_ks_, (size_t)8 * p_.ks_stride() * cap));
+    batch_cap_ = cap;
+}
+
+int Device::alloc_slot() {
+    if (!free_slots_.empty()) {
+        int s = free_slots_.back();
+        free_slots_.pop_back();
+        return s;
+    }
+    ensure_arena(next_slot_ + 1);
+    return (int)next_slot_++;
+}
+void Device::free_slot(int s) {
+    if (s >= 0) free_slots_.push_back(s);
+}
+
+void Device::write_slots(const int* slots, size_t n, const uint64_t* host) {
+    const int L = p_.lwe_len(), S = p_.slot_stride();
+    for (size_t i = 0; i < n; ++i)
+        HIP_CHECK(hipMemcpyAsync(d_arena_ + (size_t)slots[i] * S, host + i * L, 8 * (size_t)L, hipMemcpyHostToDevice, STREAM));
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+}
+void Device::read_slot(int slot, uint64_t* host) {
+    HIP_CHECK(hipMemcpyAsync(host, d_arena_ + (size_t)slot * p_.slot_stride(), 8 * (size_t)p_.lwe_len(),
+                             hipMemcpyDeviceToHost, STREAM));
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+}
+void Device::zero_slot(int slot) {
+    HIP_CHECK(hipMemsetAsync(d_arena_ + (size_t)slot * p_.slot_stride(), 0, 8 * (size_t)p_.lwe_len(), STREAM));
+}
+
+void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk) {
+    const size_t kp1 = p_.k + 1;
+    if (ksk.size() != (size_t)p_.big() * p_.ks_level * (p_.n + 1)) throw Error(FR_ERR_INVALID, "ksk size");
+    if (bsk.size() != (size_t)p_.n * kp1 * kp1 * p_.N) throw Error(FR_ERR_INVALID, "bsk size");
+    (void)hipFree(d_ksk_);
+    (void)hipFree(d_bsk_);
+    d_ksk_ = d_bsk_ = nullptr;
+    HIP_CHECK(hipMalloc(&d_ksk_, 8 * ksk.size()));
+    HIP_CHECK(hipMemcpy(d_ksk_, ksk.data(), 8 * ksk.size(), hipMemcpyHostToDevice));
+    uint64_t* coef = nullptr;
+    HIP_CHECK(hipMalloc(&coef, 8 * bsk.size()));
+    HIP_CHECK(hipMemcpy(coef, bsk.data(), 8 * bsk.size(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMalloc(&d_bsk_, 8 * bsk.size()));
+    const uint64_t n_inv = gl_pow((uint64_t)p_.N, P - 2);
+    const int blocks = p_.n * (p_.k + 1);
+    if (p_.N == 2048 && p_.k == 1)
+        k_bsk_to_ntt<2048, 1><<<blocks, 2 * 128, br_smem_bytes<2048, 1>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+    else if (p_.N == 1024 && p_.k == 2)
+        k_bsk_to_ntt<1024, 2><<<blocks, 3 * 64, br_smem_bytes<1024, 2>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+    else
+        k_bsk_to_ntt<1024, 1><<<blocks, 2 * 64, br_smem_bytes<1024, 1>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    HIP_CHECK(hipFree(coef));
+}
+
+void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
+    dim3 grid((unsigned)((n + KS_BT - 1) / KS_BT), (unsigned)((p_.n + 1 + KS_CT - 1) / KS_CT));
+    k_lincomb_keyswitch<3, 5><<<grid, 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_ksk_, p_.n,
+                                                         p_.big(), d_ks, p_.ks_stride());
+    HIP_CHECK(hipGetLastError());
+}
+
+void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
+    if (p_.N == 2048 && p_.k == 1)
+        k_blind_rotate<2048, 1><<<(unsigned)n, 256, br_smem_bytes<2048, 1>(), STREAM>>>(
+            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
+    else if (p_.N == 1024 && p_.k == 2)
+        k_blind_rotate<1024, 2><<<(unsigned)n, 192, br_smem_bytes<1024, 2>(), STREAM>>>(
+            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
+    else
+        k_blind_rotate<1024, 1><<<(unsigned)n, 128, br_smem_bytes<1024, 1>(), STREAM>>>(
+            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
+    HIP_CHECK(hipGetLastError());
+}
+
+void Device::run_level(const DevGate* gates, size_t n) {
+    if (!n) return;
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    for (size_t i = 0; i < n; ++i) {
+        const DevGate& g = gates[i];
+        if (g.n_in < 0 || g.n_in > 15 || g.out_slot < 0 || (size_t)g.out_slot >= next_slot_)
+            throw Error(FR_ERR_INVALID, "device gate: bad descriptor");
+        for (int q = 0; q < g.n_in; ++q)
+            if (g.in_slot[q] < 0 || (size_t)g.in_slot[q] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad input slot");
+    }
+    ensure_batch(n);
+    // the staging buffer may still be read by an in-flight copy
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    std::memcpy(h_gates_, gates, sizeof(DevGate) * n);
+    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof(DevGate) * n, hipMemcpyHostToDevice, STREAM));
+    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)ev_[0], STREAM));
+    launch_ks(d_gates_, n, d_ks_);
+    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)ev_[1], STREAM));
+    launch_br(d_gates_, d_ks_, n);
+    if (profiling_) {
+        HIP_CHECK(hipEventRecord((hipEvent_t)ev_[2], STREAM));
+        HIP_CHECK(hipEventSynchronize((hipEvent_t)ev_[2]));
+        float ks = 0, br = 0;
+        HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
+        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)ev_[1], (hipEvent_t)ev_[2]));
+        timers_.ks_ms += ks;
+        timers_.br_ms += br;
+        timers_.br_launches += 1;
+        timers_.br_gates += n;
+    }
+}
+
+void Device::run_linear(const DevGate& g) {
+    ensure_batch(1);
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    std::memcpy(h_gates_, &g, sizeof g);
+    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof g, hipMemcpyHostToDevice, STREAM));
+    k_linear<<<(p_.lwe_len() + 255) / 256, 256, 0, STREAM>>>(d_gates_, d_arena_, p_.slot_stride(), p_.lwe_len());
+    HIP_CHECK(hipGetLastError());
+}
+
+void Device::sync() { HIP_CHECK(hipStreamSynchronize(STREAM)); }
+
+// ---------------------------------------------------------------- tests
+void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    std::vector<int> slots(count);
+    std::vector<DevGate> gates(count);
+    for (size_t i = 0; i < count; ++i) slots[i] = alloc_slot();
+    write_slots(slots.data(), count, in);
+    for (size_t i = 0; i < count; ++i) {
+        std::memset(&gates[i], 0, sizeof(DevGate));
+        gates[i].n_in = 1;
+        gates[i].in_slot[0] = slots[i];
+        gates[i].in_w[0] = 1;
+    }
+    ensure_batch(count);
+    HIP_CHECK(hipMemcpy(d_gates_, gates.data(), sizeof(DevGate) * count, hipMemcpyHostToDevice));
+    launch_ks(d_gates_, count, d_ks_);
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    const int ks = p_.ks_stride();
+    for (size_t i = 0; i < count; ++i)
+        HIP_CHECK(hipMemcpy(out + i * (p_.n + 1), d_ks_ + i * ks, 8 * (size_t)(p_.n + 1), hipMemcpyDeviceToHost));
+    for (int s : slots) free_slot(s);
+}
+
+void Device::blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_t count, uint64_t* out) {
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    ensure_batch(count);
+    const int ks = p_.ks_stride();
+    for (size_t i = 0; i < count; ++i)
+        HIP_CHECK(hipMemcpy(d_ks_ + i * ks, ks_in + i * (p_.n + 1), 8 * (size_t)(p_.n + 1), hipMemcpyHostToDevice));
+    std::vector<int> slots(count);
+    std::vector<DevGate> gates(count);
+    for (size_t i = 0; i < count; ++i) {
+        slots[i] = alloc_slot();
+        std::memset(&gates[i], 0, sizeof(DevGate));
+        std::memcpy(gates[i].lut, luts + 16 * i, 16);
+        gates[i].out_slot = slots[i];
+    }
+    HIP_CHECK(hipMemcpy(d_gates_, gates.data(), sizeof(DevGate) * count, hipMemcpyHostToDevice));
+    launch_br(d_gates_, d_ks_, count);
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    for (size_t i = 0; i < count; ++i) read_slot(slots[i], out + i * p_.lwe_len());
+    for (int s : slots) free_slot(s);
+}
+
+void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out) {
+    const int N = p_.N;
+    uint64_t *da, *db, *dout;
+    HIP_CHECK(hipMalloc(&da, 8 * count * N));
+    HIP_CHECK(hipMalloc(&db, 8 * count * N));
+    HIP_CHECK(hipMalloc(&dout, 8 * count * N));
+    HIP_CHECK(hipMemcpy(da, a, 8 * count * N, hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(db, b, 8 * count * N, hipMemcpyHostToDevice));
+    const uint64_t n_inv = gl_pow((uint64_t)N, P - 2);
+    if (N == 2048) {
+        size_t sm = 8 * (2 * (size_t)Geom<2048>::NP + 2 * 2048);
+        HIP_CHECK(hipFuncSetAttribute((const void*)k_ring_mul<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        k_ring_mul<2048><<<(unsigned)count, 256, sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
+    } else {
+        size_t sm = 8 * (2 * (size_t)Geom<1024>::NP + 2 * 1024);
+        k_ring_mul<1024><<<(unsigned)count, 128, sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
+    }
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    HIP_CHECK(hipMemcpy(out, dout, 8 * count * N, hipMemcpyDeviceToHost));
+    (void)hipFree(da);
+    (void)hipFree(db);
+    (void)hipFree(dout);
+}
+
+void Device::bench_pbs(const std::vector<DevGate>& gates, int iters, double* br_ms, double* total_ms) {
+    const size_t n = gates.size();
+    ensure_batch(n);
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    std::memcpy(h_gates_, gates.data(), sizeof(DevGate) * n);
+    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof(DevGate) * n, hipMemcpyHostToDevice, STREAM));
+    float br_sum = 0;
+    HIP_CHECK(hipEventRecord((hipEvent_t)ev_[3], STREAM));
+    for (int it = 0; it < iters; ++it) {
+        launch_ks(d_gates_, n, d_ks_);
+        HIP_CHECK(hipEventRecord((hipEvent_t)ev_[1], STREAM));
+        launch_br(d_gates_, d_ks_, n);
+        HIP_CHECK(hipEventRecord((hipEvent_t)ev_[2], STREAM));
+        HIP_CHECK(hipEventSynchronize((hipEvent_t)ev_[2]));
+        float br = 0;
+        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)ev_[1], (hipEvent_t)ev_[2]));
+        br_sum += br;
+    }
+    HIP_CHECK(hipEventRecord((hipEvent_t)ev_[0], STREAM));
+    HIP_CHECK(hipEventSynchronize((hipEvent_t)ev_[0]));
+    float tot = 0;
+    HIP_CHECK(hipEventElapsedTime(&tot, (hipEvent_t)ev_[3], (hipEvent_t)ev_[0]));
+    *br_ms = br_sum;
+    *total_ms = tot;
+}
+
+}  // namespace fr

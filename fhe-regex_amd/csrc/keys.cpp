@@ -1,0 +1,268 @@
+// Client key parsing, deterministic server-key generation and client-side
+// encryption.  Follows tfhe-rs 0.2 shortint semantics as used by the reference
+// (src/regex/ciphertext.rs:32-45, src/regex/engine.rs:248-254): LWE encryption
+// under the big (flattened GLWE) key with glwe noise, KSK big->small under the
+// LWE noise, GGSW bootstrapping key with one 2^23 gadget level.  The GGSW ring
+// is Z_p[X]/(X^N+1), p = 2^64-2^32+1.
+#include "keys.h"
+
+#include <cmath>
+#include <cstring>
+#include <thread>
+
+namespace fr {
+
+// ---------------------------------------------------------------- ChaCha20
+static inline uint32_t rotl32(uint32_t a, int b) { return (a << b) | (a >> (32 - b)); }
+#define FR_QR(a, b, c, d)                      \
+    a += b; d ^= a; d = rotl32(d, 16);         \
+    c += d; b ^= c; b = rotl32(b, 12);         \
+    a += b; d ^= a; d = rotl32(d, 8);          \
+    c += d; b ^= c; b = rotl32(b, 7);
+
+static void chacha_block(uint64_t seed, uint64_t stream, uint64_t counter, uint32_t out[16]) {
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                             (uint32_t)seed, (uint32_t)(seed >> 32), 0x243F6A88u, 0x85A308D3u,
+                             0x13198A2Eu, 0x03707344u, 0xA4093822u, 0x299F31D0u,
+                             (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)stream,
+                             (uint32_t)(stream >> 32)};
+    uint32_t x[16];
+    std::memcpy(x, in, sizeof x);
+    for (int i = 0; i < 10; ++i) {
+        FR_QR(x[0], x[4], x[8], x[12]); FR_QR(x[1], x[5], x[9], x[13]);
+        FR_QR(x[2], x[6], x[10], x[14]); FR_QR(x[3], x[7], x[11], x[15]);
+        FR_QR(x[0], x[5], x[10], x[15]); FR_QR(x[1], x[6], x[11], x[12]);
+        FR_QR(x[2], x[7], x[8], x[13]); FR_QR(x[3], x[4], x[9], x[14]);
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+uint64_t Rng::u64(uint64_t idx) {
+    uint64_t blk = idx >> 3;
+    if (!valid_ || blk != blk_) {
+        chacha_block(seed_, stream_, blk, w_);
+        blk_ = blk;
+        valid_ = true;
+    }
+    int o = (int)(idx & 7) * 2;
+    return (uint64_t)w_[o] | ((uint64_t)w_[o + 1] << 32);
+}
+
+int64_t Rng::gaussian(uint64_t idx, double sigma) {
+    uint64_t x1 = u64(2 * idx), x2 = u64(2 * idx + 1);
+    double u1 = (double)((x1 >> 11) + 1) * 0x1.0p-53;
+    double u2 = (double)(x2 >> 11) * 0x1.0p-53;
+    double rad = std::sqrt(-2.0 * std::log(u1));
+    double z = rad * std::cos(6.283185307179586 * u2);
+    double scaled = z * (sigma * 18446744073709551616.0);
+    return (int64_t)std::llround(scaled);
+}
+
+static inline uint64_t zp_from_i64(int64_t v) {
+    return v >= 0 ? (uint64_t)v % P : P - ((uint64_t)(-v) % P);
+}
+
+// ---------------------------------------------------------------- key parse
+ClientKey parse_client_key(const uint8_t* d, size_t len) {
+    size_t off = 0;
+    auto u = [&](size_t o) -> uint64_t {
+        if (o + 8 > len) throw Error(FR_ERR_INVALID, "client key: truncated");
+        uint64_t v;
+        std::memcpy(&v, d + o, 8);
+        return v;
+    };
+    auto f = [&](size_t o) -> double {
+        uint64_t v = u(o);
+        double x;
+        std::memcpy(&x, &v, 8);
+        return x;
+    };
+    ClientKey ck;
+    uint64_t nb = u(off);
+    if (nb == 0 || nb > (1u << 20)) throw Error(FR_ERR_INVALID, "client key: bad big key length");
+    ck.s_big.resize(nb);
+    for (uint64_t i = 0; i < nb; ++i) ck.s_big[i] = u(off + 8 + 8 * i);
+    off += 8 + 8 * nb;
+    uint64_t ng = u(off);
+    off += 8 + 8 * ng;                 // GLWE key data (identical to the big key)
+    off += 8;                          // polynomial_size
+    uint64_t ns = u(off);
+    if (ns == 0 || ns > (1u << 16)) throw Error(FR_ERR_INVALID, "client key: bad small key length");
+    ck.s_small.resize(ns);
+    for (uint64_t i = 0; i < ns; ++i) ck.s_small[i] = u(off + 8 + 8 * i);
+    off += 8 + 8 * ns;
+    ck.n = (int)u(off);
+    ck.k = (int)u(off + 8);
+    ck.N = (int)u(off + 16);
+    ck.lwe_sigma = f(off + 24);
+    ck.glwe_sigma = f(off + 32);
+    ck.pbs_base_log = (int)u(off + 40);
+    ck.pbs_level = (int)u(off + 48);
+    ck.ks_base_log = (int)u(off + 56);
+    ck.ks_level = (int)u(off + 64);
+    ck.message_modulus = u(off + 112);
+    ck.carry_modulus = u(off + 120);
+    ck.num_blocks = u(off + 128);
+    if (off + 136 != len) throw Error(FR_ERR_INVALID, "client key: unexpected length");
+    for (auto b : ck.s_big)
+        if (b > 1) throw Error(FR_ERR_INVALID, "client key: non-binary big key");
+    for (auto b : ck.s_small)
+        if (b > 1) throw Error(FR_ERR_INVALID, "client key: non-binary small key");
+    if ((uint64_t)ck.n != ns || (uint64_t)ck.k * ck.N != nb)
+        throw Error(FR_ERR_INVALID, "client key: inconsistent dimensions");
+    return ck;
+}
+
+// ---------------------------------------------------------------- host NTT
+static int brv(int x, int bits) {
+    int r = 0;
+    for (int b = 0; b < bits; ++b)
+        if (x >> b & 1) r |= 1 << (bits - 1 - b);
+    return r;
+}
+
+NttTables::NttTables(int N_) : N(N_) {
+    logN = 0;
+    while ((1 << logN) < N) ++logN;
+    uint64_t psi = gl_pow(7, (P - 1) / (2 * (uint64_t)N));
+    uint64_t ipsi = gl_pow(psi, 2 * (uint64_t)N - 1);
+    zeta.resize(N);
+    izeta.resize(N);
+    for (int k = 0; k < N; ++k) {
+        zeta[k] = gl_pow(psi, (uint64_t)brv(k, logN));
+        izeta[k] = gl_pow(ipsi, (uint64_t)brv(k, logN));
+    }
+    n_inv = gl_pow((uint64_t)N, P - 2);
+}
+
+void NttTables::forward(uint64_t* a) const {
+    for (int s = 0; s < logN; ++s) {
+        int L = N >> (s + 1);
+        for (int start = 0; start < N; start += 2 * L) {
+            uint64_t z = zeta[(1 << s) + start / (2 * L)];
+            for (int j = start; j < start + L; ++j) {
+                uint64_t t = gl_mul(z, a[j + L]);
+                a[j + L] = gl_sub(a[j], t);
+                a[j] = gl_add(a[j], t);
+            }
+        }
+    }
+}
+
+void NttTables::inverse(uint64_t* a) const {
+    for (int s = logN - 1; s >= 0; --s) {
+        int L = N >> (s + 1);
+        for (int start = 0; start < N; start += 2 * L) {
+            uint64_t z = izeta[(1 << s) + start / (2 * L)];
+            for (int j = start; j < start + L; ++j) {
+                uint64_t u = a[j], v = a[j + L];
+                a[j] = gl_add(u, v);
+                a[j + L] = gl_mul(gl_sub(u, v), z);
+            }
+        }
+    }
+    for (int j = 0; j < N; ++j) a[j] = gl_mul(a[j], n_inv);
+}
+
+// ---------------------------------------------------------------- keygen
+template <class F>
+static void parallel_for(int n, F&& fn) {
+    unsigned hw = std::thread::hardware_concurrency();
+    int T = (int)(hw ? (hw > 16 ? 16 : hw) : 4);
+    if (T > n) T = n > 0 ? n : 1;
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            for (int i = t; i < n; i += T) fn(i);
+        });
+    for (auto& x : th) x.join();
+}
+
+void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& ksk) {
+    const int big = p.big(), n = p.n, L = p.ks_level, B = p.ks_base_log;
+    ksk.assign((size_t)big * L * (n + 1), 0);
+    parallel_for(big, [&](int i) {
+        Rng rm(seed, STREAM_KSK_MASK), rn(seed, STREAM_KSK_NOISE);
+        for (int j = 0; j < L; ++j) {
+            uint64_t row = (uint64_t)i * L + j;
+            uint64_t* o = ksk.data() + row * (n + 1);
+            uint64_t body = 0;
+            for (int t = 0; t < n; ++t) {
+                o[t] = rm.u64(row * n + t);
+                body += o[t] * ck.s_small[t];
+            }
+            body += ck.s_big[i] << (64 - B * (j + 1));
+            body += (uint64_t)rn.gaussian(row, p.lwe_sigma);
+            o[n] = body;
+        }
+    });
+}
+
+void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk) {
+    const int k = p.k, N = p.N, n = p.n;
+    const size_t kp1 = (size_t)k + 1;
+    bsk.assign((size_t)n * kp1 * kp1 * N, 0);
+    NttTables T(N);
+    std::vector<uint64_t> S((size_t)k * N);
+    for (int j = 0; j < k; ++j) {
+        for (int t = 0; t < N; ++t) S[(size_t)j * N + t] = ck.s_big[(size_t)j * N + t];
+        T.forward(S.data() + (size_t)j * N);
+    }
+    parallel_for(n, [&](int i) {
+        Rng rm(seed, STREAM_BSK_MASK), rn(seed, STREAM_BSK_NOISE);
+        std::vector<uint64_t> tmp(N), acc(N);
+        for (size_t r = 0; r < kp1; ++r) {
+            uint64_t* row = bsk.data() + ((size_t)i * kp1 + r) * kp1 * N;
+            std::fill(acc.begin(), acc.end(), 0);
+            for (int j = 0; j < k; ++j) {
+                uint64_t* A = row + (size_t)j * N;
+                uint64_t base = (((uint64_t)i * kp1 + r) * k + j) * N;
+                for (int t = 0; t < N; ++t) {
+                    uint64_t x = rm.u64(base + t);
+                    A[t] = x >= P ? x - P : x;
+                }
+                std::memcpy(tmp.data(), A, 8 * (size_t)N);
+                T.forward(tmp.data());
+                for (int t = 0; t < N; ++t) acc[t] = gl_add(acc[t], gl_mul(tmp[t], S[(size_t)j * N + t]));
+            }
+            T.inverse(acc.data());
+            uint64_t* Bp = row + (size_t)k * N;
+            uint64_t nb = ((uint64_t)i * kp1 + r) * N;
+            for (int t = 0; t < N; ++t) Bp[t] = gl_add(acc[t], zp_from_i64(rn.gaussian(nb + t, p.glwe_sigma)));
+            if (ck.s_small[i]) row[r * N] = gl_add(row[r * N], PBS_G);
+        }
+    });
+}
+
+// ---------------------------------------------------------------- client
+void encrypt_blocks(const Params& p, const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed,
+                    uint64_t first_block, uint64_t* out) {
+    const int big = p.big();
+    Rng rm(seed, STREAM_ENC_MASK), rn(seed, STREAM_ENC_NOISE);
+    for (size_t q = 0; q < count; ++q) {
+        uint64_t* o = out + q * (big + 1);
+        uint64_t qb = first_block + q, body = 0;
+        for (int t = 0; t < big; ++t) {
+            o[t] = rm.u64(qb * big + t);
+            body += o[t] * ck.s_big[t];
+        }
+        body += (uint64_t)msgs[q] << DELTA_LOG;
+        body += (uint64_t)rn.gaussian(qb, p.glwe_sigma);
+        o[big] = body;
+    }
+}
+
+uint64_t lwe_phase(const Params& p, const ClientKey& ck, const uint64_t* lwe) {
+    const int big = p.big();
+    uint64_t acc = lwe[big];
+    for (int t = 0; t < big; ++t) acc -= lwe[t] * ck.s_big[t];
+    return acc;
+}
+
+uint32_t decode16(uint64_t phase) {
+    const uint64_t delta = 1ULL << DELTA_LOG;
+    uint64_t rounding = (phase & (delta >> 1)) << 1;
+    return (uint32_t)(((phase + rounding) / delta) % 16);
+}
+
+}  // namespace fr

@@ -1,0 +1,72 @@
+// Client key (reference fixture layout), deterministic server-key generation,
+// client-side encryption — host C++.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "common.h"
+
+namespace fr {
+
+// ChaCha20 (DJB layout: 64-bit block counter, 64-bit stream id); key words =
+// seed (2 words) + 6 fixed constants.  u64 number idx of a stream is words
+// 2*(idx%8), 2*(idx%8)+1 of block idx/8 — random access, so keygen is
+// parallel and deterministic.
+enum Stream : uint64_t {
+    STREAM_KSK_MASK = 1,
+    STREAM_KSK_NOISE = 2,
+    STREAM_BSK_MASK = 3,
+    STREAM_BSK_NOISE = 4,
+    STREAM_ENC_MASK = 5,
+    STREAM_ENC_NOISE = 6,
+};
+
+class Rng {
+  public:
+    Rng(uint64_t seed, uint64_t stream) : seed_(seed), stream_(stream) {}
+    uint64_t u64(uint64_t idx);
+    // Box-Muller on words 2*idx, 2*idx+1; rounded to 2^-64 torus units.
+    int64_t gaussian(uint64_t idx, double sigma);
+
+  private:
+    uint64_t seed_, stream_, blk_ = 0;
+    bool valid_ = false;
+    uint32_t w_[16];
+};
+
+struct ClientKey {
+    std::vector<uint64_t> s_big;    // flattened GLWE key (2048 bits)
+    std::vector<uint64_t> s_small;  // LWE key after keyswitch (742 bits)
+    int n = 0, k = 0, N = 0;
+    int pbs_base_log = 0, pbs_level = 0, ks_base_log = 0, ks_level = 0;
+    double lwe_sigma = 0, glwe_sigma = 0;
+    uint64_t message_modulus = 0, carry_modulus = 0, num_blocks = 0;
+};
+
+// Parse the bincode RadixClientKey of the reference fixture.
+ClientKey parse_client_key(const uint8_t* data, size_t len);
+
+// KSK: [i in kN][level j][t in n+1], torus 2^64.
+void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& ksk);
+// BSK: [i in n][row r in k+1][component c in k+1][coef], coefficient domain mod P.
+void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk);
+
+// Fresh LWE encryptions of block messages (Delta = 2^59) under the big key.
+void encrypt_blocks(const Params& p, const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed,
+                    uint64_t first_block, uint64_t* out /* count * (kN+1) */);
+uint64_t lwe_phase(const Params& p, const ClientKey& ck, const uint64_t* lwe);
+// tfhe-rs shortint decrypt_message_and_carry: round(phase / Delta) mod 16
+uint32_t decode16(uint64_t phase);
+
+// Host negacyclic NTT over Z_p (merged-psi Cooley-Tukey / Gentleman-Sande,
+// bit-reversed evaluation order) — used by keygen and for device twiddles.
+struct NttTables {
+    int N = 0, logN = 0;
+    std::vector<uint64_t> zeta, izeta;  // zeta[k] = psi^brv(k), izeta[k] = psi^-brv(k)
+    uint64_t n_inv = 0;
+    explicit NttTables(int N);
+    void forward(uint64_t* a) const;
+    void inverse(uint64_t* a) const;  // includes the 1/N factor
+};
+
+}  // namespace fr

@@ -1,0 +1,480 @@
+// Value DAG -> PBS gate program.  See lower.h.
+#include "lower.h"
+
+#include <algorithm>
+#include <bitset>
+#include <map>
+#include <tuple>
+#include <cstring>
+
+namespace fr {
+
+void lut_eq(uint8_t* lut, int v) {
+    for (int x = 0; x < 16; ++x) lut[x] = (uint8_t)(x == v);
+}
+void lut_sign(uint8_t* lut, int v) {
+    for (int x = 0; x < 16; ++x) lut[x] = (uint8_t)(x < v ? 0 : (x == v ? 1 : 2));
+}
+void lut_gt3(uint8_t* lut, bool le) {
+    for (int x = 0; x < 16; ++x) {
+        int sh = x / 3, sl = x % 3;
+        bool gt = (sh == 2) || (sh == 1 && sl == 2);
+        lut[x] = (uint8_t)(le ? !gt : gt);
+    }
+}
+void lut_at_least(uint8_t* lut, int m) {
+    for (int x = 0; x < 16; ++x) lut[x] = (uint8_t)(x >= m);
+}
+
+namespace {
+
+struct Lit {
+    int gate;
+    bool neg;
+    bool operator<(const Lit& o) const { return gate != o.gate ? gate < o.gate : neg < o.neg; }
+    bool operator==(const Lit& o) const { return gate == o.gate && neg == o.neg; }
+};
+struct Form {
+    enum K { CONST, LIT, AND, OR, SET } k = CONST;
+    int c = 0;
+    Lit lit{-1, false};
+    std::vector<Lit> lits;
+    int pos = -1;           // SET: content position
+    std::bitset<256> set;   // SET: the characters for which the form is 1
+};
+
+inline int cblock(int pos, int blk) { return -(1 + pos * 4 + blk); }
+
+struct Lowerer {
+    const ValueDag& dag;
+    int mode;
+    Program prog;
+    std::map<std::vector<int64_t>, int> gate_index;  // hash-consing of gates
+    std::vector<Form> memo;
+    std::vector<char> done;
+
+    Lowerer(const ValueDag& d, int m) : dag(d), mode(m), memo(d.nodes.size()), done(d.nodes.size(), 0) {}
+
+    int add_gate(const std::vector<int64_t>& key, PGate g) {
+        auto it = gate_index.find(key);
+        if (it != gate_index.end()) return it->second;
+        prog.gates.push_back(std::move(g));
+        int id = (int)prog.gates.size() - 1;
+        gate_index[key] = id;
+        return id;
+    }
+    // [x_{2h} + 4 x_{2h+1} ? v] over the packed nibble of char `pos`
+    int nibble_gate(int kind, int pos, int half, int v, int tag) {
+        PGate g;
+        g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
+        if (kind == 0) lut_eq(g.lut, v);
+        else lut_sign(g.lut, v);
+        return add_gate({1, kind, pos, half, v, tag}, g);
+    }
+    // arbitrary 16-entry LUT over the packed nibble (x_{2h} + 4 x_{2h+1}) of char `pos`
+    int nibble_lut_gate(int pos, int half, const uint8_t* lut) {
+        PGate g;
+        g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
+        std::memcpy(g.lut, lut, 16);
+        std::vector<int64_t> key{6, pos, half};
+        for (int v = 0; v < 16; ++v) key.push_back(lut[v]);
+        return add_gate(key, g);
+    }
+    // Lower "char at pos is in S" (S != {} and S != all).  Characters split into
+    // nibbles (hi, lo); rows = hi values grouped by their lo-set, columns = lo
+    // values grouped by their hi-set.
+    //  * product set (one non-empty row class): AND{[hi in H], [lo in L]} — two
+    //    nibble PBS, mergeable into a parent AND;
+    //  * rows x cols <= 16: two class LUTs + one PBS on (cols*row + col);
+    //  * otherwise OR over row classes of AND{[hi in class], [lo in L_class]}.
+    Form lower_set(int pos, const std::bitset<256>& S) {
+        std::vector<std::bitset<16>> rowset(16);
+        for (int h = 0; h < 16; ++h)
+            for (int l = 0; l < 16; ++l)
+                if (S[h * 16 + l]) rowset[h][l] = 1;
+        // row classes: distinct non-empty lo-sets (class 0 = empty)
+        std::vector<std::bitset<16>> rc;
+        int rowcls[16];
+        for (int h = 0; h < 16; ++h) {
+            rowcls[h] = 0;
+            if (rowset[h].none()) continue;
+            int c = -1;
+            for (size_t i = 0; i < rc.size(); ++i)
+                if (rc[i] == rowset[h]) c = (int)i;
+            if (c < 0) { rc.push_back(rowset[h]); c = (int)rc.size() - 1; }
+            rowcls[h] = c + 1;
+        }
+        if (rc.size() == 1) {  // product set
+            uint8_t lh[16], ll[16];
+            bool allh = true, alll = true;
+            for (int v = 0; v < 16; ++v) {
+                lh[v] = (uint8_t)(rowcls[v] != 0);
+                ll[v] = (uint8_t)rc[0][v];
+                allh &= lh[v] != 0;
+                alll &= ll[v] != 0;
+            }
+            Form f;
+            f.k = Form::AND;
+            if (!allh) f.lits.push_back(Lit{nibble_lut_gate(pos, 1, lh), false});
+            if (!alll) f.lits.push_back(Lit{nibble_lut_gate(pos, 0, ll), false});
+            std::sort(f.lits.begin(), f.lits.end());
+            if (f.lits.size() == 1) return lit_form(f.lits[0]);
+            return f;
+        }
+        // column classes: distinct hi-sets of each lo value
+        std::vector<std::bitset<16>> cc;
+        int colcls[16];
+        for (int l = 0; l < 16; ++l) {
+            std::bitset<16> sig;
+            for (int h = 0; h < 16; ++h) sig[h] = S[h * 16 + l];
+            int c = -1;
+            for (size_t i = 0; i < cc.size(); ++i)
+                if (cc[i] == sig) c = (int)i;
+            if (c < 0) { cc.push_back(sig); c = (int)cc.size() - 1; }
+            colcls[l] = c;
+        }
+        const int R = (int)rc.size() + 1, Cn = (int)cc.size();
+        if (R * Cn <= 16) {
+            uint8_t lh[16], ll[16];
+            for (int v = 0; v < 16; ++v) {
+                lh[v] = (uint8_t)rowcls[v];
+                ll[v] = (uint8_t)colcls[v];
+            }
+            int gh = nibble_lut_gate(pos, 1, lh), gl = nibble_lut_gate(pos, 0, ll);
+            PGate g;
+            g.ins = {{gh, Cn}, {gl, 1}};
+            for (int v = 0; v < 16; ++v) {
+                int r = v / Cn, c = v % Cn;
+                // representative hi for row class r, lo for column class c
+                int member = 0;
+                if (r >= 1 && r < R)
+                    for (int l = 0; l < 16; ++l)
+                        if (colcls[l] == c) { member = rc[r - 1][l]; break; }
+                g.lut[v] = (uint8_t)member;
+            }
+            std::vector<int64_t> key{7, gh, gl, Cn};
+            for (int v = 0; v < 16; ++v) key.push_back(g.lut[v]);
+            return lit_form(Lit{add_gate(key, g), false});
+        }
+        Form f;
+        f.k = Form::OR;
+        for (size_t r = 0; r < rc.size(); ++r) {
+            uint8_t lh[16], ll[16];
+            for (int v = 0; v < 16; ++v) {
+                lh[v] = (uint8_t)(rowcls[v] == (int)r + 1);
+                ll[v] = (uint8_t)rc[r][v];
+            }
+            std::vector<Lit> a{Lit{nibble_lut_gate(pos, 1, lh), false}, Lit{nibble_lut_gate(pos, 0, ll), false}};
+            f.lits.push_back(Lit{threshold_gate(true, a), false});
+        }
+        std::sort(f.lits.begin(), f.lits.end());
+        return f;
+    }
+    // SET -> general form (cheaper of S and its complement)
+    Form expand_set(const Form& f) {
+        if (f.set.none()) return const_form(0);
+        if (f.set.all()) return const_form(1);
+        Form a = lower_set(f.pos, f.set);
+        if (a.k == Form::AND || a.k == Form::LIT) return a;
+        Form b = negate(lower_set(f.pos, ~f.set));
+        if (b.k == Form::AND || b.k == Form::LIT) return b;
+        return a;
+    }
+    // AND / OR of literals as one threshold gate (m <= MAX_FANIN)
+    int threshold_gate(bool is_and, std::vector<Lit> lits) {
+        std::sort(lits.begin(), lits.end());
+        PGate g;
+        int negs = 0;
+        std::vector<int64_t> key{2, is_and ? 1 : 0};
+        for (auto& l : lits) {
+            g.ins.push_back({l.gate, l.neg ? -1 : 1});
+            negs += l.neg;
+            key.push_back(l.gate * 2 + l.neg);
+        }
+        g.offset = negs;
+        lut_at_least(g.lut, is_and ? (int)lits.size() : 1);
+        return add_gate(key, g);
+    }
+    Lit materialize(const Form& f0) {
+        if (f0.k == Form::SET) return materialize(expand_set(f0));
+        const Form& f = f0;
+        if (f.k == Form::LIT) return f.lit;
+        if (f.k == Form::CONST) throw Error(FR_ERR_INVALID, "lowering: cannot materialize a constant");
+        bool is_and = f.k == Form::AND;
+        std::vector<Lit> lits = f.lits;
+        while ((int)lits.size() > MAX_FANIN) {
+            size_t m = lits.size();
+            size_t chunks = (m + MAX_FANIN - 1) / MAX_FANIN;
+            std::vector<Lit> next;
+            size_t start = 0;
+            for (size_t c = 0; c < chunks; ++c) {
+                size_t len = m / chunks + (c < m % chunks ? 1 : 0);
+                std::vector<Lit> part(lits.begin() + start, lits.begin() + start + len);
+                start += len;
+                next.push_back(part.size() == 1 ? part[0] : Lit{threshold_gate(is_and, part), false});
+            }
+            lits = std::move(next);
+        }
+        if (lits.size() == 1) return lits[0];
+        return Lit{threshold_gate(is_and, lits), false};
+    }
+    static Form lit_form(Lit l) {
+        Form f;
+        f.k = Form::LIT;
+        f.lit = l;
+        return f;
+    }
+    static Form const_form(int c) {
+        Form f;
+        f.k = Form::CONST;
+        f.c = c;
+        return f;
+    }
+    // literals of f as members of an AND (is_and) or OR list
+    std::vector<Lit> members(const Form& f0, bool is_and) {
+        if (f0.k == Form::SET) return members(expand_set(f0), is_and);
+        const Form& f = f0;
+        if (f.k == Form::CONST) throw Error(FR_ERR_INVALID, "lowering: constant member");
+        if (f.k == Form::LIT) return {f.lit};
+        if ((f.k == Form::AND) == is_and) return f.lits;
+        return {materialize(f)};
+    }
+    Form combine(bool is_and, const Form& a0, const Form& b0) {
+        // same-position character sets combine exactly
+        if (a0.k == Form::SET && b0.k == Form::SET && a0.pos == b0.pos) {
+            Form f = a0;
+            f.set = is_and ? (a0.set & b0.set) : (a0.set | b0.set);
+            if (f.set.none()) return const_form(0);
+            if (f.set.all()) return const_form(1);
+            return f;
+        }
+        const Form a = a0.k == Form::SET ? expand_set(a0) : a0;
+        const Form b = b0.k == Form::SET ? expand_set(b0) : b0;
+        // constant folding (booleans)
+        if (a.k == Form::CONST) return is_and ? (a.c ? b : const_form(0)) : (a.c ? const_form(1) : b);
+        if (b.k == Form::CONST) return is_and ? (b.c ? a : const_form(0)) : (b.c ? const_form(1) : a);
+        std::vector<Lit> l = members(a, is_and), r = members(b, is_and);
+        l.insert(l.end(), r.begin(), r.end());
+        std::sort(l.begin(), l.end());
+        l.erase(std::unique(l.begin(), l.end()), l.end());
+        for (size_t i = 0; i + 1 < l.size(); ++i)
+            if (l[i].gate == l[i + 1].gate) return const_form(is_and ? 0 : 1);  // x & !x, x | !x
+        if (l.size() == 1) return lit_form(l[0]);
+        Form f;
+        f.k = is_and ? Form::AND : Form::OR;
+        f.lits = std::move(l);
+        return f;
+    }
+    Form negate(const Form& f) {
+        Form g = f;
+        switch (f.k) {
+            case Form::SET: g.set = ~f.set; break;
+            case Form::CONST: g.c = f.c ^ 1; break;
+            case Form::LIT: g.lit.neg = !f.lit.neg; break;
+            case Form::AND:
+            case Form::OR:
+                g.k = f.k == Form::AND ? Form::OR : Form::AND;
+                for (auto& l : g.lits) l.neg = !l.neg;
+                break;
+        }
+        return g;
+    }
+
+    // ---------------------------------------------------------- threshold
+    Form lower_t(int id) {
+        if (done[id]) return memo[id];
+        // iterative post-order over AND/OR/NOT chains to avoid deep recursion
+        std::vector<int> st{id};
+        while (!st.empty()) {
+            int x = st.back();
+            if (done[x]) { st.pop_back(); continue; }
+            const VNode& n = dag.nodes[x];
+            bool ready = true;
+            if ((n.op == VNode::AND || n.op == VNode::OR || n.op == VNode::NOT)) {
+                if (!done[n.a]) { st.push_back(n.a); ready = false; }
+                if (n.b >= 0 && !done[n.b]) { st.push_back(n.b); ready = false; }
+            }
+            if (!ready) continue;
+            st.pop_back();
+            Form f;
+            switch (n.op) {
+                case VNode::POS: throw Error(FR_ERR_INVALID, "lowering: content char used as a boolean");
+                case VNode::CONST: f = const_form(n.c); break;
+                case VNode::EQ:
+                case VNode::GT:
+                case VNode::LE: {
+                    f.k = Form::SET;
+                    f.pos = n.pos;
+                    for (int ch = 0; ch < 256; ++ch)
+                        f.set[ch] = n.op == VNode::EQ ? ch == n.c : n.op == VNode::GT ? ch > n.c : ch <= n.c;
+                    break;
+                }
+                case VNode::AND: f = combine(true, memo[n.a], memo[n.b]); break;
+                case VNode::OR: f = combine(false, memo[n.a], memo[n.b]); break;
+                case VNode::NOT: f = negate(memo[n.a]); break;
+            }
+            memo[x] = std::move(f);
+            done[x] = 1;
+        }
+        return memo[id];
+    }
+    int cmp_gate(const VNode& n, int tag) {
+        int hi = nibble_gate(1, n.pos, 1, n.c >> 4, tag);
+        int lo = nibble_gate(1, n.pos, 0, n.c & 15, tag);
+        PGate g;
+        g.ins = {{hi, 3}, {lo, 1}};
+        lut_gt3(g.lut, n.op == VNode::LE);
+        return add_gate({3, n.op, n.pos, n.c, tag}, g);
+    }
+
+    // ---------------------------------------------------------- faithful
+    // one gate group per distinct reference op
+    Form lower_f(int id) {
+        std::vector<int> st{id};
+        while (!st.empty()) {
+            int x = st.back();
+            if (done[x]) { st.pop_back(); continue; }
+            const VNode& n = dag.nodes[x];
+            bool ready = true;
+            if ((n.op == VNode::AND || n.op == VNode::OR || n.op == VNode::NOT)) {
+                if (!done[n.a]) { st.push_back(n.a); ready = false; }
+                if (n.b >= 0 && !done[n.b]) { st.push_back(n.b); ready = false; }
+            }
+            if (!ready) continue;
+            st.pop_back();
+            Form f;
+            switch (n.op) {
+                case VNode::POS: throw Error(FR_ERR_INVALID, "lowering: content char used as a boolean");
+                case VNode::CONST: f = const_form(n.c); break;
+                case VNode::EQ: {
+                    // smart_eq: both nibble tests, then [lo + hi == 2]  (3 PBS)
+                    int lo = nibble_gate(0, n.pos, 0, n.c & 15, n.c);
+                    int hi = nibble_gate(0, n.pos, 1, n.c >> 4, n.c);
+                    PGate g;
+                    g.ins = {{lo, 1}, {hi, 1}};
+                    lut_eq(g.lut, 2);
+                    f = lit_form(Lit{add_gate({4, n.pos, n.c}, g), false});
+                    break;
+                }
+                case VNode::GT:
+                case VNode::LE: f = lit_form(Lit{cmp_gate(n, n.c), false}); break;
+                case VNode::AND:
+                case VNode::OR: {
+                    bool is_and = n.op == VNode::AND;
+                    const Form& a = memo[n.a];
+                    const Form& b = memo[n.b];
+                    PGate g;
+                    int offset = 0;
+                    std::vector<int64_t> key{5, is_and, x};
+                    for (const Form* o : {&a, &b}) {
+                        if (o->k == Form::CONST) {
+                            offset += o->c;  // trivial operand (e.g. or(false, x), execution.rs:154-164)
+                        } else {
+                            Lit l = materialize(*o);
+                            g.ins.push_back({l.gate, l.neg ? -1 : 1});
+                            offset += l.neg;
+                        }
+                    }
+                    g.offset = offset;
+                    if (is_and) lut_eq(g.lut, 2);
+                    else lut_at_least(g.lut, 1);
+                    f = lit_form(Lit{add_gate(key, g), false});
+                    break;
+                }
+                case VNode::NOT: f = negate(memo[n.a]); break;  // smart_bitxor(a, 1) on a boolean: linear
+            }
+            memo[x] = std::move(f);
+            done[x] = 1;
+        }
+        return memo[id];
+    }
+};
+
+}  // namespace
+
+void compute_levels(Program& prog) {
+    int maxl = 0;
+    std::vector<size_t> width;
+    for (auto& g : prog.gates) {
+        int l = 0;
+        for (auto& in : g.ins)
+            if (in.src >= 0) l = std::max(l, prog.gates[in.src].level);
+        g.level = l + 1;
+        maxl = std::max(maxl, g.level);
+        if ((size_t)g.level >= width.size()) width.resize(g.level + 1, 0);
+        width[g.level]++;
+    }
+    prog.levels = maxl;
+    prog.max_width = 0;
+    for (auto w : width) prog.max_width = std::max(prog.max_width, w);
+}
+
+Program lower(const ValueDag& dag, int root, int mode) {
+    Lowerer lw(dag, mode);
+    Form f = mode == FR_LOWER_FAITHFUL ? lw.lower_f(root) : lw.lower_t(root);
+    if (f.k == Form::CONST) {
+        lw.prog.out_gate = -1;
+        lw.prog.out_const = f.c;
+        lw.prog.out_w = 0;
+    } else {
+        Lit l = lw.materialize(f);
+        lw.prog.out_gate = l.gate;
+        lw.prog.out_const = l.neg ? 1 : 0;
+        lw.prog.out_w = l.neg ? -1 : 1;
+    }
+    // drop gates not reachable from the output (e.g. materialized then merged)
+    Program& p = lw.prog;
+    std::vector<char> live(p.gates.size(), 0);
+    if (p.out_gate >= 0) {
+        std::vector<int> st{p.out_gate};
+        while (!st.empty()) {
+            int g = st.back();
+            st.pop_back();
+            if (live[g]) continue;
+            live[g] = 1;
+            for (auto& in : p.gates[g].ins)
+                if (in.src >= 0 && !live[in.src]) st.push_back(in.src);
+        }
+    }
+    std::vector<int> remap(p.gates.size(), -1);
+    Program out;
+    for (size_t g = 0; g < p.gates.size(); ++g) {
+        if (!live[g]) continue;
+        PGate ng = p.gates[g];
+        for (auto& in : ng.ins)
+            if (in.src >= 0) in.src = remap[in.src];
+        remap[g] = (int)out.gates.size();
+        out.gates.push_back(std::move(ng));
+    }
+    out.out_gate = p.out_gate >= 0 ? remap[p.out_gate] : -1;
+    out.out_const = p.out_const;
+    out.out_w = p.out_w;
+    compute_levels(out);
+    return out;
+}
+
+int eval_program(const Program& prog, const uint8_t* content, size_t L) {
+    std::vector<int> val(prog.gates.size(), 0);
+    for (size_t g = 0; g < prog.gates.size(); ++g) {
+        const PGate& G = prog.gates[g];
+        int s = G.offset;
+        for (auto& in : G.ins) {
+            int v;
+            if (in.src >= 0) {
+                v = val[in.src];
+            } else {
+                int cb = -in.src - 1;
+                size_t pos = (size_t)(cb / 4);
+                if (pos >= L) throw Error(FR_ERR_INVALID, "program references content past its end");
+                v = (content[pos] >> (2 * (cb % 4))) & 3;
+            }
+            s += in.w * v;
+        }
+        if (s < 0 || s >= 16) throw Error(FR_ERR_INVALID, "program lincomb out of the 16-value message space");
+        val[g] = G.lut[s];
+    }
+    if (prog.out_gate < 0) return prog.out_const;
+    return prog.out_const + prog.out_w * val[prog.out_gate];
+}
+
+}  // namespace fr

@@ -1,0 +1,56 @@
+// Lowering of the recorded value DAG (what the reference computes through
+// tfhe-rs smart_* calls) into a program of programmable bootstraps (PBS).
+//
+// Every gate is  out = LUT( offset + sum_i w_i * in_i )  with the sum in
+// [0, 16) — one shortint-style PBS over a 16-value message space (Delta=2^59,
+// one padding bit).  Inputs are content blocks (2-bit radix digits of the
+// encrypted characters, src/regex/ciphertext.rs:18-29) or earlier gates.
+//
+// FR_LOWER_FAITHFUL: one gate group per reference op (eq/gt/le = 3 PBS, and/or
+//   = 1 PBS, not = linear), the decomposition of SURVEY App. D.3.
+// FR_LOWER_THRESHOLD (default): AND/OR trees of the recorded circuit are
+//   flattened into n-ary threshold gates (AND of m literals = [sum == m],
+//   OR = [sum >= 1], m <= 15), NOT is pushed into literals (De Morgan, linear),
+//   equality nibble tests are shared across constants.  Same decrypted result,
+//   far fewer PBS and levels.
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "regex.h"
+
+namespace fr {
+
+struct PIn {
+    int32_t src;  // >= 0: gate index; < 0: content block -(1 + pos*4 + blk)
+    int32_t w;
+};
+struct PGate {
+    std::vector<PIn> ins;
+    int32_t offset = 0;
+    uint8_t lut[16] = {0};
+    int32_t level = 0;
+};
+struct Program {
+    std::vector<PGate> gates;
+    // result = out_const + out_w * gates[out_gate]   (out_gate == -1: constant)
+    int32_t out_gate = -1, out_const = 0, out_w = 0;
+    int32_t levels = 0;
+    size_t max_width = 0;
+};
+
+constexpr int MAX_FANIN = 15;
+
+Program lower(const ValueDag& dag, int root, int mode);
+// Plaintext semantics of a program (LUT semantics, with the [0,16) range
+// check); returns the result value.
+int eval_program(const Program& prog, const uint8_t* content, size_t L);
+void compute_levels(Program& prog);
+
+// LUT builders
+void lut_eq(uint8_t* lut, int v);     // [x == v]
+void lut_sign(uint8_t* lut, int v);   // x < v -> 0, x == v -> 1, x > v -> 2
+void lut_gt3(uint8_t* lut, bool le);  // over 3*s_hi + s_lo: gt (or its negation)
+void lut_at_least(uint8_t* lut, int m);
+
+}  // namespace fr

@@ -1,0 +1,587 @@
+// Host C++ restatement of the reference regex layer.
+//   parser:      src/regex/parser.rs:146-351 (combine 4.6.6 commit semantics)
+//   enumerator:  src/regex/engine.rs:45-214
+//   driver:      src/regex/engine.rs:8-42
+//   Execution:   src/regex/execution.rs:64-222
+#include "regex.h"
+
+#include <sstream>
+
+namespace fr {
+
+// =================================================================== AST
+std::string to_string(const Re& r) {
+    std::ostringstream o;
+    switch (r.kind) {
+        case Re::SOF: o << "SOF"; break;
+        case Re::EOF_: o << "EOF"; break;
+        case Re::ANY: o << "Any"; break;
+        case Re::CHAR: o << "Char(" << (int)r.c << ")"; break;
+        case Re::BETWEEN: o << "Between(" << (int)r.from << "," << (int)r.to << ")"; break;
+        case Re::RANGE:
+            o << "Range(";
+            for (size_t i = 0; i < r.cs.size(); ++i) o << (i ? "," : "") << (int)r.cs[i];
+            o << ")";
+            break;
+        case Re::NOT: o << "Not(" << to_string(*r.a) << ")"; break;
+        case Re::EITHER: o << "Either(" << to_string(*r.a) << "," << to_string(*r.b) << ")"; break;
+        case Re::OPTIONAL: o << "Optional(" << to_string(*r.a) << ")"; break;
+        case Re::REPEATED:
+            o << "Repeated(" << to_string(*r.a) << ",";
+            if (r.has_lo) o << r.lo; else o << "_";
+            o << ",";
+            if (r.has_hi) o << r.hi; else o << "_";
+            o << ")";
+            break;
+        case Re::SEQ:
+            o << "Seq(";
+            for (size_t i = 0; i < r.xs.size(); ++i) o << (i ? "," : "") << to_string(*r.xs[i]);
+            o << ")";
+            break;
+    }
+    return o.str();
+}
+
+static ReP mk(Re::Kind k) {
+    auto r = std::make_shared<Re>();
+    r->kind = k;
+    return r;
+}
+static ReP mk_char(uint8_t c) {
+    auto r = std::make_shared<Re>();
+    r->kind = Re::CHAR;
+    r->c = c;
+    return r;
+}
+
+// case_insensitive, parser.rs:44-81: only Char is folded.
+static ReP fold_case(const ReP& n) {
+    auto r = std::make_shared<Re>(*n);
+    switch (n->kind) {
+        case Re::CHAR: {
+            r->kind = Re::RANGE;
+            uint8_t c = n->c;
+            r->cs = {c};
+            if (c >= 'a' && c <= 'z') r->cs.push_back((uint8_t)(c - 32));
+            else if (c >= 'A' && c <= 'Z') r->cs.push_back((uint8_t)(c + 32));
+            break;
+        }
+        case Re::NOT:
+        case Re::OPTIONAL:
+        case Re::REPEATED: r->a = fold_case(n->a); break;
+        case Re::EITHER: r->a = fold_case(n->a); r->b = fold_case(n->b); break;
+        case Re::SEQ:
+            for (auto& x : r->xs) x = fold_case(x);
+            break;
+        default: break;
+    }
+    return r;
+}
+
+// =============================================================== parser
+// Every rule returns {ok, committed, pos, node}: combine's "consumed" status.
+// choice/many/optional propagate committed errors; attempt() clears them.
+namespace {
+struct PR {
+    bool ok = false;
+    bool committed = false;
+    size_t pos = 0;
+    ReP node;
+};
+inline PR ok(ReP n, size_t p) { PR r; r.ok = true; r.pos = p; r.node = std::move(n); return r; }
+inline PR fail(bool committed) { PR r; r.committed = committed; return r; }
+
+struct Parser {
+    const std::string& s;
+    explicit Parser(const std::string& str) : s(str) {}
+    bool at(size_t i, char ch) const { return i < s.size() && s[i] == ch; }
+    static bool letter(unsigned char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
+    static bool nonesc(unsigned char c) {  // parser.rs:252-254
+        static const char* syms = "&;:,`~-_!@#%'\"";
+        for (const char* p = syms; *p; ++p)
+            if ((unsigned char)*p == c) return true;
+        return false;
+    }
+    bool is_letter(size_t i) const { return i < s.size() && letter((unsigned char)s[i]); }
+    bool is_digit(size_t i) const { return i < s.size() && s[i] >= '0' && s[i] <= '9'; }
+
+    static uint64_t parse_digits(const std::string& d) {  // parser.rs:349-351
+        if (d.empty()) throw Error(FR_ERR_REF_PANIC, "parse_digits: empty digit string (reference panics)");
+        unsigned __int128 v = 0;
+        for (char ch : d) {
+            v = v * 10 + (unsigned)(ch - '0');
+            if (v >> 64) throw Error(FR_ERR_REF_PANIC, "parse_digits: usize overflow (reference panics)");
+        }
+        return (uint64_t)v;
+    }
+
+    // regex := attempt(term '|' regex) | term           (parser.rs:208-222)
+    PR regex(size_t i) {
+        PR t = term(i);
+        if (t.ok && at(t.pos, '|')) {
+            PR r = regex(t.pos + 1);
+            if (r.ok) {
+                auto e = mk(Re::EITHER);
+                auto m = std::const_pointer_cast<Re>(e);
+                m->a = t.node;
+                m->b = r.node;
+                return ok(e, r.pos);
+            }
+        }
+        return term(i);
+    }
+    // term := many(factor); one factor is returned unwrapped (parser.rs:224-236)
+    PR term(size_t i) {
+        std::vector<ReP> xs;
+        size_t j = i;
+        for (;;) {
+            PR f = factor(j);
+            if (!f.ok) {
+                if (f.committed) return fail(true);
+                break;
+            }
+            xs.push_back(f.node);
+            j = f.pos;
+        }
+        if (xs.size() == 1) return ok(xs[0], j);
+        auto q = std::make_shared<Re>();
+        q->kind = Re::SEQ;
+        q->xs = std::move(xs);
+        return ok(q, j);
+    }
+    // factor := attempt(atom '?') | attempt(repeated) | atom   (parser.rs:238-250)
+    PR factor(size_t i) {
+        {
+            PR a = atom(i);
+            if (a.ok && at(a.pos, '?')) {
+                auto q = std::make_shared<Re>();
+                q->kind = Re::OPTIONAL;
+                q->a = a.node;
+                return ok(q, a.pos + 1);
+            }
+        }
+        {
+            PR r = repeated(i);
+            if (r.ok) return r;
+        }
+        return atom(i);
+    }
+    // atom (parser.rs:256-269)
+    PR atom(size_t i) {
+        if (at(i, '.')) return ok(mk(Re::ANY), i + 1);
+        if (at(i, '\\') && i + 1 < s.size()) return ok(mk_char((uint8_t)s[i + 1]), i + 2);
+        if (i < s.size() && (letter((unsigned char)s[i]) || nonesc((unsigned char)s[i])))
+            return ok(mk_char((uint8_t)s[i]), i + 1);
+        if (at(i, '[')) {
+            PR r = range(i + 1);
+            if (!r.ok) return fail(true);
+            if (!at(r.pos, ']')) return fail(true);
+            return ok(r.node, r.pos + 1);
+        }
+        if (at(i, '(')) {
+            PR r = regex(i + 1);
+            if (!r.ok) return fail(true);
+            if (!at(r.pos, ')')) return fail(true);
+            return ok(r.node, r.pos + 1);
+        }
+        return fail(false);
+    }
+    // range (parser.rs:279-294)
+    PR range(size_t i) {
+        if (at(i, '^')) {
+            PR r = range(i + 1);
+            if (!r.ok) return fail(true);
+            auto q = std::make_shared<Re>();
+            q->kind = Re::NOT;
+            q->a = r.node;
+            return ok(q, r.pos);
+        }
+        if (is_letter(i) && at(i + 1, '-') && is_letter(i + 2)) {
+            auto q = std::make_shared<Re>();
+            q->kind = Re::BETWEEN;
+            q->from = (uint8_t)s[i];
+            q->to = (uint8_t)s[i + 2];
+            return ok(q, i + 3);
+        }
+        if (is_letter(i)) {
+            auto q = std::make_shared<Re>();
+            q->kind = Re::RANGE;
+            size_t j = i;
+            while (is_letter(j)) q->cs.push_back((uint8_t)s[j++]);
+            return ok(q, j);
+        }
+        return fail(false);
+    }
+    // repeated (parser.rs:296-347); always called under attempt() by factor,
+    // so only success or panic is observable.
+    PR repeated(size_t i) {
+        {  // attempt(atom ('*'|'+'))
+            PR a = atom(i);
+            if (a.ok && (at(a.pos, '*') || at(a.pos, '+'))) {
+                auto q = std::make_shared<Re>();
+                q->kind = Re::REPEATED;
+                q->a = a.node;
+                if (s[a.pos] == '+') { q->has_lo = true; q->lo = 1; }
+                return ok(q, a.pos + 1);
+            }
+        }
+        {  // attempt(atom '{' digits '}')
+            PR a = atom(i);
+            if (a.ok && at(a.pos, '{')) {
+                size_t j = a.pos + 1;
+                std::string d;
+                while (is_digit(j)) d.push_back(s[j++]);
+                if (at(j, '}')) {
+                    uint64_t n = parse_digits(d);
+                    auto q = std::make_shared<Re>();
+                    q->kind = Re::REPEATED;
+                    q->a = a.node;
+                    q->has_lo = q->has_hi = true;
+                    q->lo = q->hi = n;
+                    return ok(q, j + 1);
+                }
+            }
+        }
+        {  // atom '{' digits? ',' digits? '}'
+            PR a = atom(i);
+            if (!a.ok) return fail(a.committed);
+            if (!at(a.pos, '{')) return fail(true);
+            size_t j = a.pos + 1;
+            std::string lo, hi;
+            while (is_digit(j)) lo.push_back(s[j++]);
+            if (!at(j, ',')) return fail(true);
+            ++j;
+            while (is_digit(j)) hi.push_back(s[j++]);
+            if (!at(j, '}')) return fail(true);
+            auto q = std::make_shared<Re>();
+            q->kind = Re::REPEATED;
+            q->a = a.node;
+            if (!lo.empty()) { q->has_lo = true; q->lo = parse_digits(lo); }
+            if (!hi.empty()) { q->has_hi = true; q->hi = parse_digits(hi); }
+            return ok(q, j + 1);
+        }
+    }
+};
+}  // namespace
+
+ReP parse(const std::string& pattern) {
+    Parser ps(pattern);
+    const std::string& s = pattern;
+    size_t i = 0;
+    if (!ps.at(0, '/')) throw Error(FR_ERR_PARSE, "failed to parse regular expression");
+    i = 1;
+    bool sof = false, eof = false;
+    if (ps.at(i, '^')) { sof = true; ++i; }
+    PR r = ps.regex(i);
+    if (!r.ok) throw Error(FR_ERR_PARSE, "failed to parse regular expression");
+    i = r.pos;
+    if (ps.at(i, '$')) { eof = true; ++i; }
+    if (!ps.at(i, '/')) throw Error(FR_ERR_PARSE, "failed to parse regular expression");
+    ++i;
+    bool ci = false;
+    if (ps.at(i, 'i')) { ci = true; ++i; }
+    ReP re = r.node;
+    if (sof || eof) {
+        auto q = std::make_shared<Re>();
+        q->kind = Re::SEQ;
+        if (sof) q->xs.push_back(mk(Re::SOF));
+        q->xs.push_back(re);
+        if (eof) q->xs.push_back(mk(Re::EOF_));
+        re = q;
+    }
+    if (ci) re = fold_case(re);
+    if (i != s.size())
+        throw Error(FR_ERR_PARSE, "failed to parse regular expression, unexpected token at start of: " + s.substr(i));
+    return re;
+}
+
+// ============================================================ value DAG
+static inline uint64_t mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9e3779b97f4a7c15ULL + (h << 6) + (h >> 2);
+    return h;
+}
+
+int ValueDag::add(const VNode& n) {
+    uint64_t h = mix(mix(mix(mix(mix(0, n.op), (uint64_t)(int64_t)n.a), (uint64_t)(int64_t)n.b), (uint64_t)n.pos), n.c);
+    auto& bucket = index_[h];
+    for (int id : bucket) {
+        const VNode& m = nodes[id];
+        if (m.op == n.op && m.a == n.a && m.b == n.b && m.pos == n.pos && m.c == n.c) return id;
+    }
+    nodes.push_back(n);
+    bucket.push_back((int)nodes.size() - 1);
+    return (int)nodes.size() - 1;
+}
+
+int ValueDag::eval(int id, const uint8_t* content, std::vector<int16_t>& memo) const {
+    if (memo.size() < nodes.size()) memo.resize(nodes.size(), -1);
+    // iterative post-order to avoid deep recursion on long OR chains
+    std::vector<int> st{id};
+    while (!st.empty()) {
+        int x = st.back();
+        if (memo[x] >= 0) { st.pop_back(); continue; }
+        const VNode& n = nodes[x];
+        bool ready = true;
+        if (n.a >= 0 && memo[n.a] < 0) { st.push_back(n.a); ready = false; }
+        if (n.b >= 0 && memo[n.b] < 0) { st.push_back(n.b); ready = false; }
+        if (!ready) continue;
+        int v = 0;
+        switch (n.op) {
+            case VNode::POS: v = content[n.pos]; break;
+            case VNode::CONST: v = n.c; break;
+            case VNode::EQ: v = content[n.pos] == n.c; break;
+            case VNode::GT: v = content[n.pos] > n.c; break;
+            case VNode::LE: v = content[n.pos] <= n.c; break;
+            case VNode::AND: v = memo[n.a] & memo[n.b]; break;
+            case VNode::OR: v = memo[n.a] | memo[n.b]; break;
+            case VNode::NOT: v = memo[n.a] ^ 1; break;
+        }
+        memo[x] = (int16_t)v;
+        st.pop_back();
+    }
+    return memo[id];
+}
+
+// ============================================================ Execution
+int Execution::key(Tag t, int64_t a, int64_t b) {
+    uint64_t h = mix(mix(mix(0, t), (uint64_t)a), (uint64_t)b);
+    auto& bucket = key_index_[h];
+    for (int id : bucket) {
+        const KeyRec& k = keys_[id];
+        if (k.t == t && k.a == a && k.b == b) return id;
+    }
+    keys_.push_back({t, a, b});
+    bucket.push_back((int)keys_.size() - 1);
+    return (int)keys_.size() - 1;
+}
+int Execution::const_of(int k) const { return keys_[k].t == K_CONST ? (int)keys_[k].a : -1; }
+
+template <class F>
+Val Execution::with_cache(int k, F&& f) {  // execution.rs:212-222
+    auto it = cache_.find(k);
+    if (it != cache_.end()) {
+        ++cache_hits_;
+        return {it->second, k};
+    }
+    ++ct_ops_;
+    int v = f();
+    cache_[k] = v;
+    return {v, k};
+}
+
+Val Execution::ct_constant(uint8_t c) {  // execution.rs:197-210
+    VNode n{VNode::CONST};
+    n.c = c;
+    return {dag_.add(n), key(K_CONST, c)};
+}
+Val Execution::ct_pos(int at) {
+    VNode n{VNode::POS};
+    n.pos = at;
+    return {dag_.add(n), key(K_POS, at)};
+}
+
+static VNode cmp_node(VNode::Op op, const ValueDag& d, const Val& a, const Val& b) {
+    const VNode& x = d.nodes[a.value];
+    const VNode& y = d.nodes[b.value];
+    if (x.op != VNode::POS || y.op != VNode::CONST)
+        throw Error(FR_ERR_INVALID, "comparison operands must be (content char, constant)");
+    VNode n{op};
+    n.pos = x.pos;
+    n.c = y.c;
+    return n;
+}
+
+Val Execution::ct_eq(const Val& a, const Val& b) {  // execution.rs:64-79
+    int k = key(K_EQ, a.key, b.key);
+    return with_cache(k, [&] { return dag_.add(cmp_node(VNode::EQ, dag_, a, b)); });
+}
+Val Execution::ct_ge(const Val& a, const Val& b) {  // execution.rs:81-96 (smart_gt)
+    int k = key(K_GE, a.key, b.key);
+    return with_cache(k, [&] { return dag_.add(cmp_node(VNode::GT, dag_, a, b)); });
+}
+Val Execution::ct_le(const Val& a, const Val& b) {  // execution.rs:98-113
+    int k = key(K_LE, a.key, b.key);
+    return with_cache(k, [&] { return dag_.add(cmp_node(VNode::LE, dag_, a, b)); });
+}
+Val Execution::ct_and(const Val& a, const Val& b) {  // execution.rs:115-146
+    int k = key(K_AND, a.key, b.key);
+    int ca = const_of(a.key), cb = const_of(b.key);
+    if (ca == 1) return {b.value, k};
+    if (ca == 0) return {a.value, k};
+    if (cb == 1) return {a.value, k};
+    if (cb == 0) return {b.value, k};
+    return with_cache(k, [&] {
+        VNode n{VNode::AND};
+        n.a = a.value;
+        n.b = b.value;
+        return dag_.add(n);
+    });
+}
+Val Execution::ct_or(const Val& a, const Val& b) {  // execution.rs:148-176
+    int k = key(K_OR, a.key, b.key);
+    int ca = const_of(a.key), cb = const_of(b.key);
+    if (ca == 1) return {a.value, k};
+    if (cb == 1) return {b.value, k};
+    if (ca == 0 && cb == 0) return {a.value, k};
+    return with_cache(k, [&] {
+        VNode n{VNode::OR};
+        n.a = a.value;
+        n.b = b.value;
+        return dag_.add(n);
+    });
+}
+Val Execution::ct_not(const Val& a) {  // execution.rs:178-195
+    int k = key(K_NOT, a.key);
+    return with_cache(k, [&] {
+        VNode n{VNode::NOT};
+        n.a = a.value;
+        return dag_.add(n);
+    });
+}
+
+// ============================================================ enumerator
+static Lazy lazy(std::function<Val(Execution&)> f) {
+    return std::make_shared<const std::function<Val(Execution&)>>(std::move(f));
+}
+static Lazy seq_and(const Lazy& prev, const Lazy& x) {  // engine.rs:197-205
+    return lazy([prev, x](Execution& ex) {
+        Val rp = (*prev)(ex);
+        Val rx = (*x)(ex);
+        return ex.ct_and(rp, rx);
+    });
+}
+
+std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
+    switch (re->kind) {  // engine.rs:51-67
+        case Re::SOF:
+            if (p == 0) return {{lazy([](Execution& ex) { return ex.ct_true(); }), p}};
+            return {};
+        case Re::EOF_:
+            if (p == L) return {{lazy([](Execution& ex) { return ex.ct_true(); }), p}};
+            return {};
+        default: break;
+    }
+    if (p >= L) return {};  // engine.rs:69-71
+    switch (re->kind) {
+        case Re::CHAR: {  // :74-80
+            uint8_t c = re->c;
+            int at = (int)p;
+            return {{lazy([c, at](Execution& ex) { return ex.ct_eq(ex.ct_pos(at), ex.ct_constant(c)); }), p + 1}};
+        }
+        case Re::ANY:  // :81
+            return {{lazy([](Execution& ex) { return ex.ct_true(); }), p + 1}};
+        case Re::NOT: {  // :82-93
+            std::vector<Branch> out;
+            for (auto& br : build_branches(L, re->a, p)) {
+                Lazy f = br.f;
+                out.push_back({lazy([f](Execution& ex) { return ex.ct_not((*f)(ex)); }), br.end});
+            }
+            return out;
+        }
+        case Re::EITHER: {  // :94-98
+            auto l = build_branches(L, re->a, p);
+            auto r = build_branches(L, re->b, p);
+            l.insert(l.end(), r.begin(), r.end());
+            return l;
+        }
+        case Re::BETWEEN: {  // :99-111
+            uint8_t f = re->from, t = re->to;
+            int at = (int)p;
+            return {{lazy([f, t, at](Execution& ex) {
+                         Val cf = ex.ct_constant(f);
+                         Val ctt = ex.ct_constant(t);
+                         Val ge = ex.ct_ge(ex.ct_pos(at), cf);
+                         Val le = ex.ct_le(ex.ct_pos(at), ctt);
+                         return ex.ct_and(ge, le);
+                     }),
+                     p + 1}};
+        }
+        case Re::RANGE: {  // :112-126
+            std::vector<uint8_t> cs = re->cs;
+            int at = (int)p;
+            return {{lazy([cs, at](Execution& ex) {
+                         Val res = ex.ct_eq(ex.ct_pos(at), ex.ct_constant(cs[0]));
+                         for (size_t i = 1; i < cs.size(); ++i) {
+                             Val e = ex.ct_eq(ex.ct_pos(at), ex.ct_constant(cs[i]));
+                             res = ex.ct_or(res, e);
+                         }
+                         return res;
+                     }),
+                     p + 1}};
+        }
+        case Re::REPEATED: {  // :127-183
+            uint64_t at_least = re->has_lo ? re->lo : 0;
+            uint64_t at_most = re->has_hi ? re->hi : (uint64_t)(L - p);
+            if (at_least > at_most) return {};
+            std::vector<std::vector<Branch>> res;
+            if (at_least == 0) res.push_back({{lazy([](Execution& ex) { return ex.ct_true(); }), p}});
+            else res.push_back({});
+            {
+                auto q = std::make_shared<Re>();
+                q->kind = Re::SEQ;
+                uint64_t reps = at_least > 1 ? at_least : 1;
+                if (reps > (1u << 24)) throw Error(FR_ERR_REF_PANIC, "repetition count too large (reference exhausts memory)");
+                for (uint64_t r = 0; r < reps; ++r) q->xs.push_back(re->a);
+                res.push_back(build_branches(L, q, p));
+            }
+            // (at_least+1 ..= at_most): each step extends the previous list;
+            // once a step yields nothing all later ones do too.
+            for (uint64_t it = at_least + 1; it <= at_most; ++it) {
+                std::vector<Branch> nxt;
+                for (auto& bp : res.back())
+                    for (auto& bx : build_branches(L, re->a, bp.end)) nxt.push_back({seq_and(bp.f, bx.f), bx.end});
+                bool empty = nxt.empty();
+                res.push_back(std::move(nxt));
+                if (empty) break;
+            }
+            std::vector<Branch> out;
+            for (auto& v : res) out.insert(out.end(), v.begin(), v.end());
+            return out;
+        }
+        case Re::OPTIONAL: {  // :184-188
+            auto out = build_branches(L, re->a, p);
+            out.push_back({lazy([](Execution& ex) { return ex.ct_true(); }), p});
+            return out;
+        }
+        case Re::SEQ: {  // :189-211
+            if (re->xs.empty()) throw Error(FR_ERR_REF_PANIC, "Seq{[]}: index out of bounds (reference panics, engine.rs:189-190)");
+            auto conts = build_branches(L, re->xs[0], p);
+            for (size_t i = 1; i < re->xs.size(); ++i) {
+                std::vector<Branch> nxt;
+                for (auto& bp : conts)
+                    for (auto& bx : build_branches(L, re->xs[i], bp.end)) nxt.push_back({seq_and(bp.f, bx.f), bx.end});
+                conts = std::move(nxt);
+            }
+            return conts;
+        }
+        default: break;
+    }
+    throw Error(FR_ERR_REF_PANIC, "unmatched regex variant");
+}
+
+Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi) {
+    ReP re = parse(pattern);  // engine.rs:13
+    if (hi > L) hi = L;
+    std::vector<Lazy> branches;
+    for (size_t i = lo; i < hi; ++i)  // engine.rs:15-18
+        for (auto& b : build_branches(L, re, i)) branches.push_back(b.f);
+    Execution ex(dag);
+    Val res;
+    if (branches.size() <= 1) {  // engine.rs:22-26
+        res = branches.empty() ? ex.ct_false() : (*branches[0])(ex);
+    } else {  // engine.rs:27-34
+        res = (*branches[0])(ex);
+        for (size_t i = 1; i < branches.size(); ++i) {
+            Val r = (*branches[i])(ex);
+            res = ex.ct_or(res, r);
+        }
+    }
+    Recorded out;
+    out.root = res.value;
+    out.ct_ops = ex.ct_operations_count();
+    out.cache_hits = ex.cache_hits();
+    out.n_branches = branches.size();
+    return out;
+}
+
+}  // namespace fr

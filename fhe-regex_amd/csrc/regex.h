@@ -1,0 +1,105 @@
+// Regex AST, parser, variant enumerator and symbolic Execution — host C++
+// restatement of the reference's src/regex/{parser,engine,execution}.rs.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "common.h"
+
+namespace fr {
+
+// ------------------------------------------------------------------ AST
+// enum RegExpr, src/regex/parser.rs:8-41
+struct Re;
+using ReP = std::shared_ptr<const Re>;
+struct Re {
+    enum Kind { SOF, EOF_, ANY, CHAR, BETWEEN, RANGE, NOT, EITHER, OPTIONAL, REPEATED, SEQ } kind;
+    uint8_t c = 0, from = 0, to = 0;
+    std::vector<uint8_t> cs;
+    ReP a, b;
+    bool has_lo = false, has_hi = false;
+    uint64_t lo = 0, hi = 0;
+    std::vector<ReP> xs;
+};
+// canonical string form (shared with oracle/regex_oracle.py)
+std::string to_string(const Re& r);
+// parse(pattern): parser.rs:146-185.  Throws Error(FR_ERR_PARSE) for the
+// reference's Err, Error(FR_ERR_REF_PANIC) where the reference panics.
+ReP parse(const std::string& pattern);
+
+// ------------------------------------------------------------ value DAG
+// What the reference actually computes homomorphically: one node per distinct
+// computation (hash-consed); short-circuited ops return an operand's node.
+struct VNode {
+    enum Op : uint8_t { POS, CONST, EQ, GT, LE, AND, OR, NOT } op;
+    int32_t a = -1, b = -1;  // operand value ids (AND/OR/NOT)
+    int32_t pos = 0;         // POS / EQ / GT / LE: content position
+    uint8_t c = 0;           // CONST value, or the comparison constant
+};
+
+struct ValueDag {
+    std::vector<VNode> nodes;
+    int add(const VNode& n);
+    int eval(int id, const uint8_t* content, std::vector<int16_t>& memo) const;
+  private:
+    std::unordered_map<uint64_t, std::vector<int>> index_;
+};
+
+// ------------------------------------------------------- Execution (symbolic)
+// src/regex/execution.rs:8-223: Executed keys (hash-consed), op cache,
+// constant short-circuits, ct_ops / cache_hits.
+struct Val {
+    int32_t value;  // ValueDag id
+    int32_t key;    // Executed key id
+};
+
+class Execution {
+  public:
+    explicit Execution(ValueDag& dag) : dag_(dag) {}
+    Val ct_eq(const Val& a, const Val& b);
+    Val ct_ge(const Val& a, const Val& b);  // smart_gt (execution.rs:93 quirk)
+    Val ct_le(const Val& a, const Val& b);
+    Val ct_and(const Val& a, const Val& b);
+    Val ct_or(const Val& a, const Val& b);
+    Val ct_not(const Val& a);
+    Val ct_constant(uint8_t c);
+    Val ct_true() { return ct_constant(1); }
+    Val ct_false() { return ct_constant(0); }
+    Val ct_pos(int at);
+    uint64_t ct_operations_count() const { return ct_ops_; }
+    uint64_t cache_hits() const { return cache_hits_; }
+
+  private:
+    enum Tag : uint8_t { K_CONST, K_POS, K_AND, K_OR, K_EQ, K_GE, K_LE, K_NOT };
+    int key(Tag t, int64_t a, int64_t b = -1);
+    int const_of(int key) const;  // -1 if not a Constant key
+    template <class F>
+    Val with_cache(int key, F&& f);
+    ValueDag& dag_;
+    std::unordered_map<uint64_t, std::vector<int>> key_index_;
+    struct KeyRec { Tag t; int64_t a, b; };
+    std::vector<KeyRec> keys_;
+    std::unordered_map<int, int> cache_;  // key -> value
+    uint64_t ct_ops_ = 0, cache_hits_ = 0;
+};
+
+using Lazy = std::shared_ptr<const std::function<Val(Execution&)>>;
+struct Branch {
+    Lazy f;
+    size_t end;
+};
+// build_branches, src/regex/engine.rs:45-214 (content only enters via its length)
+std::vector<Branch> build_branches(size_t L, const ReP& re, size_t pos);
+
+struct Recorded {
+    int root = -1;  // value id of the result
+    uint64_t ct_ops = 0, cache_hits = 0, n_branches = 0;
+};
+// has_match, src/regex/engine.rs:8-42 (start offsets restricted to [lo, hi))
+Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi);
+
+}  // namespace fr

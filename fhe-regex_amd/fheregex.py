@@ -1,0 +1,403 @@
+"""Python mirror of the reference's regex API over the MI355X C-ABI (libfheregex.so).
+
+Reference API (RKlompUU/fhe-regex) -> here:
+  src/regex/ciphertext.rs:42-45  gen_keys()                    -> gen_keys(...)
+  src/regex/ciphertext.rs:32-40  encrypt_str(ck, s)            -> ClientKey.encrypt_str(s)
+  src/regex/ciphertext.rs:8-30   create_trivial_radix(sk, m)   -> ServerKey.create_trivial_radix(m)
+  src/regex/engine.rs:8-42       has_match(sk, content, pat)   -> has_match(sk, content, pat)
+  RadixClientKey::decrypt                                      -> ClientKey.decrypt(ct)
+  src/regex/parser.rs:146-185    parse(pattern)                -> parse(pattern) (canonical AST string)
+
+Errors mirror the reference: a pattern the reference rejects raises ``ParseError``
+(reference: ``Err``), a pattern/content on which the reference panics raises
+``ReferencePanic``, non-ASCII content raises ``ValueError`` (ciphertext.rs:33-35).
+
+All homomorphic work runs in the HIP kernels behind the C-ABI; there is no CPU
+fallback: a GPU op on a context without a device raises ``NoDevice``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfheregex.so")
+REPO = os.path.dirname(HERE)
+HEADER = os.path.join(REPO, "include", "fheregex.h")
+
+FR_OK = 0
+ERR_INVALID, ERR_PARSE, ERR_REF_PANIC, ERR_NO_DEVICE, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_NON_ASCII = range(-1, -9, -1)
+LOWER_FAITHFUL, LOWER_THRESHOLD = 0, 1
+NULL_CT = 0xFFFFFFFF
+
+
+class FheRegexError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+class ParseError(FheRegexError):
+    pass
+
+
+class ReferencePanic(FheRegexError):
+    pass
+
+
+class NoDevice(FheRegexError):
+    pass
+
+
+class Params(C.Structure):
+    _fields_ = [("k", C.c_int32), ("N", C.c_int32), ("n", C.c_int32), ("ks_base_log", C.c_int32),
+                ("ks_level", C.c_int32), ("pbs_base_log", C.c_int32), ("pbs_level", C.c_int32),
+                ("_pad", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
+
+
+class MatchStats(C.Structure):
+    _fields_ = [("ct_ops", C.c_uint64), ("cache_hits", C.c_uint64), ("n_branches", C.c_uint64),
+                ("pbs", C.c_uint64), ("levels", C.c_uint64), ("max_level_width", C.c_uint64),
+                ("host_ms", C.c_double), ("device_ms", C.c_double), ("br_kernel_ms", C.c_double),
+                ("ks_kernel_ms", C.c_double), ("br_launches", C.c_uint64), ("br_gates", C.c_uint64)]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_}
+
+
+class PlainResult(C.Structure):
+    _fields_ = [("ct_ops", C.c_uint64), ("cache_hits", C.c_uint64), ("n_branches", C.c_uint64),
+                ("pbs", C.c_uint64), ("levels", C.c_uint64), ("max_level_width", C.c_uint64),
+                ("result_recorded", C.c_int32), ("result_lowered", C.c_int32)]
+
+
+class Gate(C.Structure):
+    _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("in_", C.c_uint32 * 15),
+                ("in_block", C.c_int8 * 15), ("in_w", C.c_int8 * 15), ("lut", C.c_uint8 * 16),
+                ("out", C.c_uint32)]
+
+
+u64p = C.POINTER(C.c_uint64)
+_lib = None
+
+# every exported symbol of include/fheregex.h, with (restype, argtypes)
+_SIGS = {
+    "fr_ctx_create": (C.c_int, [C.POINTER(Params), C.c_int, C.POINTER(C.c_void_p)]),
+    "fr_ctx_destroy": (C.c_int, [C.c_void_p]),
+    "fr_last_error": (C.c_char_p, []),
+    "fr_default_params": (C.c_int, [C.POINTER(Params)]),
+    "fr_load_client_key": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "fr_gen_server_key": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "fr_export_server_key": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
+    "fr_server_key_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "fr_encrypt_str": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint64, u64p]),
+    "fr_encrypt_blocks": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64, C.c_uint64, u64p]),
+    "fr_decrypt_radix": (C.c_int, [C.c_void_p, u64p, u64p]),
+    "fr_decode_block": (C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_uint32)]),
+    "fr_upload_radix": (C.c_int, [C.c_void_p, u64p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "fr_upload_bool": (C.c_int, [C.c_void_p, u64p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "fr_download_radix": (C.c_int, [C.c_void_p, C.c_uint32, u64p]),
+    "fr_release": (C.c_int, [C.c_void_p, C.c_uint32]),
+    "fr_trivial": (C.c_int, [C.c_void_p, C.c_uint8, C.POINTER(C.c_uint32)]),
+    "fr_eq_const": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint32)]),
+    "fr_gt_const": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint32)]),
+    "fr_le_const": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint8, C.POINTER(C.c_uint32)]),
+    "fr_and": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "fr_or": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "fr_not": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "fr_or_many": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_uint32)]),
+    "fr_run_gates": (C.c_int, [C.c_void_p, C.POINTER(Gate), C.c_size_t]),
+    "fr_has_match": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.POINTER(C.c_uint32),
+                               C.POINTER(MatchStats)]),
+    "fr_has_match_range": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t,
+                                     C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
+    "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "fr_plain_match": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32,
+                                 C.POINTER(PlainResult)]),
+    "fr_set_lowering": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_dev_keyswitch": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p]),
+    "fr_dev_blind_rotate": (C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_uint8), C.c_size_t, u64p]),
+    "fr_dev_ring_mul": (C.c_int, [C.c_void_p, u64p, u64p, C.c_size_t, u64p]),
+    "fr_dev_bench_pbs": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_int32,
+                                   C.POINTER(C.c_double), C.POINTER(C.c_double)]),
+    "fr_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "fr_debug_scalar": (C.c_uint64, [C.c_int32, C.c_uint64, C.c_uint64]),
+}
+
+
+def lib():
+    """Load the in-tree libfheregex.so (fails loudly if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(f"{LIB_PATH} missing: run `make -C {HERE}` (or __graft_entry__.build())")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _check(rc: int):
+    if rc == FR_OK:
+        return
+    msg = lib().fr_last_error().decode(errors="replace")
+    cls = {ERR_PARSE: ParseError, ERR_REF_PANIC: ReferencePanic, ERR_NO_DEVICE: NoDevice}.get(rc, FheRegexError)
+    if rc == ERR_NON_ASCII:
+        raise ValueError(msg)
+    raise cls(rc, msg)
+
+
+def _p(a: np.ndarray):
+    assert a.dtype == np.uint64 and a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(u64p)
+
+
+def default_params(k: Optional[int] = None, N: Optional[int] = None) -> Params:
+    p = Params()
+    _check(lib().fr_default_params(C.byref(p)))
+    if k is not None:
+        p.k = k
+    if N is not None:
+        p.N = N
+    return p
+
+
+def parse(pattern: str) -> str:
+    buf = C.create_string_buffer(1 << 16)
+    _check(lib().fr_parse(pattern.encode("latin-1"), buf, len(buf)))
+    return buf.value.decode()
+
+
+def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESHOLD,
+                start_lo: int = 0, start_hi: Optional[int] = None) -> PlainResult:
+    """Host-only symbolic run: reference counters + plaintext result of the
+    recorded circuit and of the lowered PBS program."""
+    if isinstance(content, str):
+        content = content.encode("latin-1")
+    hi = len(content) if start_hi is None else start_hi
+    r = PlainResult()
+    _check(lib().fr_plain_match(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, C.byref(r)))
+    return r
+
+
+class Context:
+    """One fr_ctx: params, keys, device arena.  device=-1: host-only."""
+
+    def __init__(self, device: int = 0, params: Optional[Params] = None):
+        self.params = params if params is not None else default_params()
+        h = C.c_void_p()
+        _check(lib().fr_ctx_create(C.byref(self.params), device, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.big = self.params.k * self.params.N
+        self.lwe_len = self.big + 1
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib().fr_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def info(self) -> str:
+        buf = C.create_string_buffer(256)
+        _check(lib().fr_device_info(self.h, buf, 256))
+        return buf.value.decode()
+
+    # keys
+    def load_client_key(self, blob: bytes):
+        _check(lib().fr_load_client_key(self.h, blob, len(blob)))
+
+    def gen_server_key(self, seed: int):
+        _check(lib().fr_gen_server_key(self.h, seed))
+
+    def export_server_key(self):
+        a, b = C.c_size_t(), C.c_size_t()
+        _check(lib().fr_server_key_sizes(self.h, C.byref(a), C.byref(b)))
+        ksk = np.zeros(a.value, dtype=np.uint64)
+        bsk = np.zeros(b.value, dtype=np.uint64)
+        _check(lib().fr_export_server_key(self.h, _p(ksk), len(ksk), _p(bsk), len(bsk)))
+        return ksk, bsk
+
+    def set_lowering(self, mode: int):
+        _check(lib().fr_set_lowering(self.h, mode))
+
+    def set_profiling(self, on: bool):
+        _check(lib().fr_set_profiling(self.h, int(on)))
+
+    # client side
+    def encrypt_str(self, s: bytes | str, seed: int) -> np.ndarray:
+        if isinstance(s, str):
+            s = s.encode("latin-1")
+        out = np.zeros((len(s), 4, self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_encrypt_str(self.h, s, len(s), seed, _p(out)))
+        return out
+
+    def encrypt_blocks(self, msgs, seed: int, first_block: int = 0) -> np.ndarray:
+        m = np.ascontiguousarray(np.asarray(msgs, dtype=np.uint8))
+        out = np.zeros((len(m), self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_encrypt_blocks(self.h, m.ctypes.data_as(C.POINTER(C.c_uint8)), len(m), seed, first_block, _p(out)))
+        return out
+
+    def decrypt_radix(self, blocks: np.ndarray) -> int:
+        b = np.ascontiguousarray(blocks, dtype=np.uint64)
+        v = C.c_uint64()
+        _check(lib().fr_decrypt_radix(self.h, _p(b), C.byref(v)))
+        return v.value
+
+    def decode_block(self, lwe: np.ndarray) -> int:
+        b = np.ascontiguousarray(lwe, dtype=np.uint64)
+        v = C.c_uint32()
+        _check(lib().fr_decode_block(self.h, _p(b), C.byref(v)))
+        return v.value
+
+    # arena
+    def upload_radix(self, blocks: np.ndarray) -> List[int]:
+        b = np.ascontiguousarray(blocks.reshape(-1, 4, self.lwe_len), dtype=np.uint64)
+        out = (C.c_uint32 * b.shape[0])()
+        _check(lib().fr_upload_radix(self.h, _p(b), b.shape[0], out))
+        return list(out)
+
+    def upload_bool(self, lwes: np.ndarray) -> List[int]:
+        b = np.ascontiguousarray(lwes.reshape(-1, self.lwe_len), dtype=np.uint64)
+        out = (C.c_uint32 * b.shape[0])()
+        _check(lib().fr_upload_bool(self.h, _p(b), b.shape[0], out))
+        return list(out)
+
+    def download_radix(self, h: int) -> np.ndarray:
+        out = np.zeros((4, self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_download_radix(self.h, h, _p(out)))
+        return out
+
+    def release(self, h: int):
+        _check(lib().fr_release(self.h, h))
+
+    def trivial(self, v: int) -> int:
+        out = C.c_uint32()
+        _check(lib().fr_trivial(self.h, v, C.byref(out)))
+        return out.value
+
+    # eager ops (the smart_* replacements)
+    def _op1c(self, fn, a, c):
+        out = C.c_uint32()
+        _check(fn(self.h, a, c, C.byref(out)))
+        return out.value
+
+    def eq_const(self, a, c): return self._op1c(lib().fr_eq_const, a, c)
+    def gt_const(self, a, c): return self._op1c(lib().fr_gt_const, a, c)
+    def le_const(self, a, c): return self._op1c(lib().fr_le_const, a, c)
+    def and_(self, a, b): return self._op1c(lib().fr_and, a, b)
+    def or_(self, a, b): return self._op1c(lib().fr_or, a, b)
+
+    def not_(self, a):
+        out = C.c_uint32()
+        _check(lib().fr_not(self.h, a, C.byref(out)))
+        return out.value
+
+    def or_many(self, hs: Sequence[int]) -> int:
+        arr = (C.c_uint32 * len(hs))(*hs)
+        out = C.c_uint32()
+        _check(lib().fr_or_many(self.h, arr, len(hs), C.byref(out)))
+        return out.value
+
+    def run_gates(self, gates: Sequence[Gate]) -> List[int]:
+        arr = (Gate * len(gates))(*gates)
+        _check(lib().fr_run_gates(self.h, arr, len(gates)))
+        return [g.out for g in arr]
+
+    def has_match(self, content: Sequence[int], pattern: str, start_lo: Optional[int] = None,
+                  start_hi: Optional[int] = None):
+        arr = (C.c_uint32 * len(content))(*content)
+        out = C.c_uint32()
+        st = MatchStats()
+        if start_lo is None and start_hi is None:
+            _check(lib().fr_has_match(self.h, arr, len(content), pattern.encode("latin-1"), C.byref(out), C.byref(st)))
+        else:
+            lo = 0 if start_lo is None else start_lo
+            hi = len(content) if start_hi is None else start_hi
+            _check(lib().fr_has_match_range(self.h, arr, len(content), pattern.encode("latin-1"), lo, hi,
+                                            C.byref(out), C.byref(st)))
+        return out.value, st
+
+    # single-stage device entry points
+    def dev_keyswitch(self, lwes: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(lwes.reshape(-1, self.lwe_len), dtype=np.uint64)
+        out = np.zeros((a.shape[0], self.params.n + 1), dtype=np.uint64)
+        _check(lib().fr_dev_keyswitch(self.h, _p(a), a.shape[0], _p(out)))
+        return out
+
+    def dev_blind_rotate(self, ks: np.ndarray, luts) -> np.ndarray:
+        a = np.ascontiguousarray(ks.reshape(-1, self.params.n + 1), dtype=np.uint64)
+        l = np.ascontiguousarray(np.asarray(luts, dtype=np.uint8).reshape(a.shape[0], 16))
+        out = np.zeros((a.shape[0], self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_dev_blind_rotate(self.h, _p(a), l.ctypes.data_as(C.POINTER(C.c_uint8)), a.shape[0], _p(out)))
+        return out
+
+    def dev_ring_mul(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(a.reshape(-1, self.params.N), dtype=np.uint64)
+        b = np.ascontiguousarray(b.reshape(-1, self.params.N), dtype=np.uint64)
+        out = np.zeros_like(a)
+        _check(lib().fr_dev_ring_mul(self.h, _p(a), _p(b), a.shape[0], _p(out)))
+        return out
+
+    def dev_bench_pbs(self, handles: Sequence[int], iters: int):
+        arr = (C.c_uint32 * len(handles))(*handles)
+        br, tot = C.c_double(), C.c_double()
+        _check(lib().fr_dev_bench_pbs(self.h, arr, len(handles), iters, C.byref(br), C.byref(tot)))
+        return br.value, tot.value
+
+
+# ------------------------------------------------------------- reference API
+@dataclass
+class ClientKey:
+    ctx: Context
+
+    def encrypt_str(self, s: str, seed: int = 0) -> List[int]:
+        """encrypt_str (ciphertext.rs:32-40) + upload: one radix handle per char."""
+        if any(ord(ch) > 127 for ch in s):
+            raise ValueError("content contains non-ascii characters")
+        return self.ctx.upload_radix(self.ctx.encrypt_str(s, seed))
+
+    def decrypt(self, ct: int) -> int:
+        return self.ctx.decrypt_radix(self.ctx.download_radix(ct))
+
+
+@dataclass
+class ServerKey:
+    ctx: Context
+
+    def create_trivial_radix(self, msg: int) -> int:
+        return self.ctx.trivial(msg)
+
+
+def gen_keys(client_key_blob: bytes, seed: int = 0, device: int = 0, params: Optional[Params] = None):
+    """gen_keys (ciphertext.rs:42-45) for a given client key: the server key is
+    derived deterministically from `seed` (ServerKey::new, engine.rs:252)."""
+    ctx = Context(device, params)
+    ctx.load_client_key(client_key_blob)
+    ctx.gen_server_key(seed)
+    return ClientKey(ctx), ServerKey(ctx)
+
+
+def has_match(sk: ServerKey, content: Sequence[int], pattern: str) -> int:
+    """engine.rs:8-42: returns the encrypted 0/1 result handle."""
+    out, _ = sk.ctx.has_match(content, pattern)
+    return out
+
+
+def header_symbols() -> List[str]:
+    import re
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"\b(fr_[a-z_]+)\s*\(", txt)) - {"fr_ctx", "FR_GATE_REF"})

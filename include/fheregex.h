@@ -1,0 +1,205 @@
+/*
+ * fheregex.h — C-ABI of the MI355X-native gate-bootstrap executor under the
+ * homomorphic regex engine of RKlompUU/fhe-regex.
+ *
+ * The boundary sits exactly where the reference's Execution layer calls into
+ * tfhe-rs (the `tfhe::integer::ServerKey` it owns):
+ *
+ *   reference call site (src/regex/...)              replaced by
+ *   ------------------------------------------------ ---------------------------
+ *   execution.rs:76   sk.smart_eq(ct_char, ct_const)  fr_eq_const
+ *   execution.rs:93   sk.smart_gt(ct_char, ct_const)  fr_gt_const   (ct_ge quirk)
+ *   execution.rs:110  sk.smart_le(ct_char, ct_const)  fr_le_const
+ *   execution.rs:143  sk.smart_bitand(a, b)           fr_and
+ *   execution.rs:173  sk.smart_bitor(a, b)            fr_or
+ *   execution.rs:190  sk.smart_bitxor(a, trivial 1)   fr_not
+ *   ciphertext.rs:8-30 create_trivial_radix(sk, m)    fr_trivial
+ *   ciphertext.rs:42-45 gen_keys_radix(PARAM_MESSAGE_2_CARRY_2, 4)
+ *                     / engine.rs:250-252 bincode client key + ServerKey::new
+ *                                                     fr_load_client_key + fr_gen_server_key
+ *   ciphertext.rs:32-40 encrypt_str / RadixClientKey::encrypt
+ *                                                     fr_encrypt_str (client side, test/bench)
+ *   mod.rs:17 / engine.rs:289 RadixClientKey::decrypt fr_decrypt_radix (client side)
+ *   engine.rs:8-42    has_match(sk, content, pattern) fr_has_match (whole engine, batched)
+ *
+ * Conventions: every function returns FR_OK (0) or a negative FR_ERR_* code;
+ * the message of the last error on this thread is fr_last_error().  No C++
+ * exception crosses the ABI.  Ciphertexts are opaque handles (fr_ct) into a
+ * device arena owned by the context; inputs are never mutated and every op
+ * writes a fresh handle (the reference always passes clones,
+ * execution.rs:74-76).  One fr_ctx per GPU, driven by one host thread.
+ * Host buffers are caller-owned and copied in or out.
+ *
+ * LWE layout on the wire: (k*N + 1) little-endian u64 per block, mask then
+ * body, torus 2^64, under the reference's flattened GLWE ("big") key; a radix
+ * ciphertext is 4 such blocks, least significant 2-bit digit first
+ * (ciphertext.rs:18-29).
+ */
+#ifndef FHEREGEX_H
+#define FHEREGEX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+    FR_OK = 0,
+    FR_ERR_INVALID = -1,      /* bad argument / handle */
+    FR_ERR_PARSE = -2,        /* pattern does not parse: reference returns Err (engine.rs:13) */
+    FR_ERR_REF_PANIC = -3,    /* the reference would panic (parser.rs:349-351, engine.rs:189-190) */
+    FR_ERR_NO_DEVICE = -4,    /* GPU op on a host-only context, or the HIP device is unusable */
+    FR_ERR_HIP = -5,          /* HIP runtime error */
+    FR_ERR_NO_KEY = -6,       /* client or server key missing */
+    FR_ERR_OOM = -7,          /* arena / allocation exhausted */
+    FR_ERR_NON_ASCII = -8,    /* encrypt_str on non-ASCII content (ciphertext.rs:33-35) */
+};
+
+typedef struct fr_ctx fr_ctx;
+typedef uint32_t fr_ct; /* ciphertext handle: a radix (4 blocks), boolean (block 0 + zeros) or trivial */
+
+typedef struct {
+    int32_t k;            /* GLWE dimension (reference: 1)            */
+    int32_t N;            /* polynomial size (reference: 2048)        */
+    int32_t n;            /* small LWE dimension (742)                */
+    int32_t ks_base_log;  /* 3 */
+    int32_t ks_level;     /* 5 */
+    int32_t pbs_base_log; /* 23 */
+    int32_t pbs_level;    /* 1 */
+    int32_t _pad;
+    double lwe_sigma;
+    double glwe_sigma;
+} fr_params;
+
+typedef struct {
+    uint64_t ct_ops;        /* reference Execution::ct_operations_count (execution.rs:56-58) */
+    uint64_t cache_hits;    /* reference Execution::cache_hits (execution.rs:60-62) */
+    uint64_t n_branches;    /* variants enumerated by build_branches (engine.rs:15-18) */
+    uint64_t pbs;           /* gate bootstraps actually executed */
+    uint64_t levels;        /* dependent PBS levels (launch batches) */
+    uint64_t max_level_width;
+    double host_ms;         /* parse + enumerate + record + lower */
+    double device_ms;       /* device execution, wall */
+    double br_kernel_ms;    /* sum of blind-rotation kernel durations (HIP events) */
+    double ks_kernel_ms;    /* sum of lincomb+keyswitch kernel durations (HIP events) */
+    uint64_t br_launches;
+    uint64_t br_gates;      /* bootstraps across all blind-rotation launches */
+} fr_match_stats;
+
+/* ----- context ----- */
+/* device >= 0: HIP device ordinal; device == -1: host-only context (parse,
+ * record, plan, keygen, plaintext evaluation; GPU ops return FR_ERR_NO_DEVICE). */
+int fr_ctx_create(const fr_params* params, int device, fr_ctx** out);
+int fr_ctx_destroy(fr_ctx* ctx);
+const char* fr_last_error(void);
+int fr_default_params(fr_params* out); /* PARAM_MESSAGE_2_CARRY_2, k=1, N=2048 */
+
+/* ----- keys ----- */
+/* bincode RadixClientKey (tfhe-rs 0.2 layout, reference test_data/client_key). */
+int fr_load_client_key(fr_ctx* ctx, const uint8_t* bincode, size_t len);
+/* Deterministic server key (KSK mod 2^64, BSK mod p) from the client key and a
+ * seed (ServerKey::new, engine.rs:252); uploads it and converts the BSK to the
+ * NTT domain on the device when the context has one. */
+int fr_gen_server_key(fr_ctx* ctx, uint64_t seed);
+/* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = n*(k+1)^2*N u64
+ * (coefficient domain mod p, layout [i][row][component][coef]).  Either may be NULL. */
+int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
+int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len);
+
+/* ----- client side (tests / bench; not on the timed path) ----- */
+int fr_encrypt_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, uint64_t* out /* len*4*(kN+1) */);
+int fr_encrypt_blocks(fr_ctx* ctx, const uint8_t* msgs, size_t count, uint64_t seed, uint64_t first_block,
+                      uint64_t* out /* count*(kN+1) */);
+int fr_decrypt_radix(fr_ctx* ctx, const uint64_t* blocks /* 4*(kN+1) */, uint64_t* value);
+int fr_decode_block(fr_ctx* ctx, const uint64_t* lwe, uint32_t* msg_and_carry);
+
+/* ----- ciphertext arena ----- */
+int fr_upload_radix(fr_ctx* ctx, const uint64_t* blocks /* n*4*(kN+1) */, size_t n, fr_ct* out /* n */);
+int fr_upload_bool(fr_ctx* ctx, const uint64_t* lwe /* n*(kN+1) */, size_t n, fr_ct* out);
+int fr_download_radix(fr_ctx* ctx, fr_ct h, uint64_t* out /* 4*(kN+1) */);
+int fr_release(fr_ctx* ctx, fr_ct h);
+int fr_trivial(fr_ctx* ctx, uint8_t value, fr_ct* out);
+
+/* ----- eager gate ops: one call per reference smart_* call ----- */
+int fr_eq_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out);
+int fr_gt_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out);
+int fr_le_const(fr_ctx* ctx, fr_ct a, uint8_t c, fr_ct* out);
+int fr_and(fr_ctx* ctx, fr_ct a, fr_ct b, fr_ct* out);
+int fr_or(fr_ctx* ctx, fr_ct a, fr_ct b, fr_ct* out);
+int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out);
+/* OR of n boolean ciphertexts (multi-GPU partial-result reduction). */
+int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out);
+
+/* ----- batched gate program ----- */
+/* One programmable bootstrap: out = PBS_lut(offset*Delta + sum_i w_i * in_i),
+ * inputs are boolean/radix-block handles (block index in_block[i] of in[i]). */
+typedef struct {
+    int32_t n_in;
+    int32_t offset;
+    fr_ct in[15];
+    int8_t in_block[15];
+    int8_t in_w[15];
+    uint8_t lut[16];
+    fr_ct out; /* filled by fr_run_gates: a fresh boolean handle */
+} fr_gate;
+/* Runs n gates; a gate may consume the output of an earlier gate in the same
+ * call by referencing FR_GATE_REF(j) as its input handle.  Level-scheduled
+ * into batched device launches. */
+#define FR_GATE_REF(j) (0x80000000u | (uint32_t)(j))
+int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n);
+
+/* ----- the engine (engine.rs:8-42) ----- */
+/* Enumerate, record, lower and execute has_match over content handles.  The
+ * result is a boolean radix handle (decrypts to 0/1).  Pattern errors return
+ * FR_ERR_PARSE / FR_ERR_REF_PANIC like the reference. */
+int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, fr_ct* out,
+                 fr_match_stats* stats);
+/* Same, restricted to start offsets [start_lo, start_hi) — the per-GPU shard of
+ * the start-offset partition (the OR over shards equals has_match). */
+int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
+                       size_t start_hi, fr_ct* out, fr_match_stats* stats);
+
+/* ----- host-only introspection (tests; no device needed) ----- */
+/* Canonical AST string of parse(pattern) (parser.rs:146-185). */
+int fr_parse(const char* pattern, char* buf, size_t buflen);
+/* Symbolic has_match over a plaintext content string: reference counters and
+ * the plaintext result of the recorded circuit and of the lowered PBS program. */
+typedef struct {
+    uint64_t ct_ops, cache_hits, n_branches;
+    uint64_t pbs, levels, max_level_width;
+    int32_t result_recorded; /* value of the recorded reference op DAG */
+    int32_t result_lowered;  /* value of the lowered PBS program (plaintext LUT semantics) */
+} fr_plain_result;
+int fr_plain_match(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
+                   int32_t lowering, fr_plain_result* out);
+
+/* lowering modes for fr_plain_match / fr_set_lowering */
+enum { FR_LOWER_FAITHFUL = 0, FR_LOWER_THRESHOLD = 1 };
+int fr_set_lowering(fr_ctx* ctx, int32_t mode);
+/* Device profiling with HIP events around every launch (adds a sync per level). */
+int fr_set_profiling(fr_ctx* ctx, int32_t on);
+
+/* ----- single-stage device entry points (parity tests of each kernel) ----- */
+/* in: count*(kN+1) torus LWEs -> out: count*(n+1) keyswitched LWEs */
+int fr_dev_keyswitch(fr_ctx* ctx, const uint64_t* in, size_t count, uint64_t* out);
+/* in: count*(n+1) keyswitched LWEs, luts: count*16 -> out: count*(kN+1) */
+int fr_dev_blind_rotate(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, size_t count, uint64_t* out);
+/* negacyclic product in Z_p[X]/(X^N+1) through the device NTT: count pairs */
+int fr_dev_ring_mul(fr_ctx* ctx, const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out);
+/* Full timed PBS batch for roofline measurement: count gates of the given
+ * lut over the uploaded boolean/radix handles; returns BR kernel ms. */
+int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, double* br_ms, double* total_ms);
+
+int fr_device_info(fr_ctx* ctx, char* buf, size_t buflen);
+
+/* Scalar maps shared by host and device code (test hook): op 0 = Z_p product
+ * x*y, 1 = PBS gadget digit of x (Z_p), 2 = Z_p -> 2^64 torus of x,
+ * 3 = modulus switch of x to 2^y, 4 = keyswitch digit y (0..4) of x (signed, as u64). */
+uint64_t fr_debug_scalar(int32_t op, uint64_t x, uint64_t y);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,219 @@
+"""ORACLE — TEST INFRASTRUCTURE ONLY (ctypes binding of oracle/build/liboracle.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this.
+Also holds an independent numpy parser of the reference fixture key
+(test_data/client_key, bincode 1.3.3 layout) so that the
+product's C++ parser is cross-checked against a second implementation.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+P_GOLDILOCKS = 0xFFFFFFFF00000001
+
+
+class Params(C.Structure):
+    _fields_ = [("k", C.c_int32), ("N", C.c_int32), ("n", C.c_int32), ("ks_base_log", C.c_int32),
+                ("ks_level", C.c_int32), ("pbs_base_log", C.c_int32), ("pbs_level", C.c_int32),
+                ("_pad", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
+
+
+class Gate(C.Structure):
+    _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("in_idx", C.c_int32 * 16),
+                ("in_w", C.c_int32 * 16), ("lut", C.c_uint8 * 16)]
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        u64p = C.POINTER(C.c_uint64)
+        L.or_gl_mul.restype = C.c_uint64
+        L.or_gl_mul.argtypes = [C.c_uint64, C.c_uint64]
+        L.or_rng_u64.restype = C.c_uint64
+        L.or_rng_u64.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
+        L.or_gaussian.restype = C.c_int64
+        L.or_gaussian.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64, C.c_double]
+        L.or_ring_mul.argtypes = [C.c_int, u64p, u64p, u64p]
+        L.or_ring_mul_schoolbook.argtypes = [C.c_int, u64p, u64p, u64p]
+        L.or_decompose_pbs.restype = C.c_uint64
+        L.or_decompose_pbs.argtypes = [C.c_uint64]
+        L.or_conv.restype = C.c_uint64
+        L.or_conv.argtypes = [C.c_uint64]
+        L.or_ks_decompose.argtypes = [C.c_uint64, C.c_int, C.c_int, C.POINTER(C.c_int32)]
+        L.or_mod_switch.restype = C.c_uint32
+        L.or_mod_switch.argtypes = [C.c_uint64, C.c_int]
+        L.or_keygen_ksk.argtypes = [C.POINTER(Params), u64p, u64p, C.c_uint64, u64p]
+        L.or_keygen_bsk.argtypes = [C.POINTER(Params), u64p, u64p, C.c_uint64, u64p]
+        L.or_encrypt.argtypes = [C.POINTER(Params), u64p, C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64, C.c_uint64, u64p]
+        L.or_phase.argtypes = [C.c_int, u64p, u64p, C.c_size_t, u64p]
+        L.or_decode16.restype = C.c_uint32
+        L.or_decode16.argtypes = [C.c_uint64]
+        L.or_keyswitch.argtypes = [C.POINTER(Params), u64p, u64p, C.c_size_t, u64p]
+        L.or_bsk_prepare.restype = C.c_void_p
+        L.or_bsk_prepare.argtypes = [C.POINTER(Params), u64p]
+        L.or_bsk_free.argtypes = [C.c_void_p]
+        L.or_blind_rotate.argtypes = [C.c_void_p, u64p, C.POINTER(C.c_uint8), u64p]
+        L.or_lincomb.argtypes = [C.c_int, C.POINTER(Gate), u64p, u64p]
+        L.or_gates.argtypes = [C.c_void_p, u64p, C.POINTER(Gate), C.c_size_t, u64p, u64p]
+        L.or_num_threads.restype = C.c_int
+        L.or_set_threads.argtypes = [C.c_int]
+        _lib = L
+    return _lib
+
+
+def ptr(a: np.ndarray, t=C.c_uint64):
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+# ----------------------------------------------------------- fixture key parse
+def parse_client_key(blob: bytes) -> dict:
+    """Second, independent parser of the bincode RadixClientKey."""
+    u = lambda off: struct.unpack_from("<Q", blob, off)[0]
+    n_big = u(0)
+    s_big = np.frombuffer(blob, dtype="<u8", count=n_big, offset=8).copy()
+    off = 8 + 8 * n_big
+    n_glwe = u(off)
+    glwe = np.frombuffer(blob, dtype="<u8", count=n_glwe, offset=off + 8).copy()
+    off += 8 + 8 * n_glwe
+    poly_size = u(off); off += 8
+    n_small = u(off)
+    s_small = np.frombuffer(blob, dtype="<u8", count=n_small, offset=off + 8).copy()
+    off += 8 + 8 * n_small
+    lwe_dim, glwe_dim, N = u(off), u(off + 8), u(off + 16)
+    lwe_sigma, glwe_sigma = struct.unpack_from("<dd", blob, off + 24)
+    pbs_base_log, pbs_level, ks_base_log, ks_level = (u(off + 40), u(off + 48), u(off + 56), u(off + 64))
+    msg_mod, carry_mod = u(off + 112), u(off + 120)
+    num_blocks = u(off + 128)
+    assert off + 136 == len(blob)
+    return dict(s_big=s_big, glwe=glwe, poly_size=poly_size, s_small=s_small, n=lwe_dim, k=glwe_dim, N=N,
+                lwe_sigma=lwe_sigma, glwe_sigma=glwe_sigma, pbs_base_log=pbs_base_log, pbs_level=pbs_level,
+                ks_base_log=ks_base_log, ks_level=ks_level, message_modulus=msg_mod, carry_modulus=carry_mod,
+                num_blocks=num_blocks)
+
+
+def params_from_key(key: dict, k: int | None = None, N: int | None = None) -> Params:
+    """Reference params (k=1, N=2048) or the k=2, N=1024 reinterpretation of the
+    same 2048-bit flattened GLWE key."""
+    k = int(key["k"]) if k is None else k
+    N = int(key["N"]) if N is None else N
+    assert k * N == len(key["s_big"])
+    return Params(k, N, int(key["n"]), int(key["ks_base_log"]), int(key["ks_level"]),
+                  int(key["pbs_base_log"]), int(key["pbs_level"]), 0, float(key["lwe_sigma"]),
+                  float(key["glwe_sigma"]))
+
+
+class Oracle:
+    """Keys + helpers around liboracle for a parameter set."""
+
+    def __init__(self, key: dict, seed: int, k: int | None = None, N: int | None = None, with_bsk=True):
+        self.key = key
+        self.P = params_from_key(key, k, N)
+        self.seed = seed
+        self.big = self.P.k * self.P.N
+        self.n = self.P.n
+        L = lib()
+        self.s_big = np.ascontiguousarray(key["s_big"], dtype=np.uint64)
+        self.s_small = np.ascontiguousarray(key["s_small"], dtype=np.uint64)
+        self.ksk = np.zeros(self.big * self.P.ks_level * (self.n + 1), dtype=np.uint64)
+        L.or_keygen_ksk(C.byref(self.P), ptr(self.s_big), ptr(self.s_small), seed, ptr(self.ksk))
+        self.bsk = None
+        self._pk = None
+        if with_bsk:
+            kp1 = self.P.k + 1
+            self.bsk = np.zeros(self.n * kp1 * kp1 * self.P.N, dtype=np.uint64)
+            L.or_keygen_bsk(C.byref(self.P), ptr(self.s_big), ptr(self.s_small), seed, ptr(self.bsk))
+            self._pk = L.or_bsk_prepare(C.byref(self.P), ptr(self.bsk))
+
+    def __del__(self):
+        if getattr(self, "_pk", None):
+            lib().or_bsk_free(self._pk)
+            self._pk = None
+
+    # -- client side
+    def encrypt_blocks(self, msgs, seed: int, first_block: int = 0) -> np.ndarray:
+        m = np.ascontiguousarray(np.asarray(msgs, dtype=np.uint8))
+        out = np.zeros((len(m), self.big + 1), dtype=np.uint64)
+        lib().or_encrypt(C.byref(self.P), ptr(self.s_big), ptr(m, C.c_uint8), len(m), seed, first_block, ptr(out))
+        return out
+
+    def encrypt_str(self, s: bytes, seed: int) -> np.ndarray:
+        """Radix encoding of src/regex/ciphertext.rs:18-29 (base-4 digits, LSB first)."""
+        msgs = [(b >> (2 * i)) & 3 for b in s for i in range(4)]
+        return self.encrypt_blocks(msgs, seed).reshape(len(s), 4, self.big + 1)
+
+    def trivial_blocks(self, msgs) -> np.ndarray:
+        m = np.asarray(msgs, dtype=np.uint64)
+        out = np.zeros((len(m), self.big + 1), dtype=np.uint64)
+        out[:, -1] = m << np.uint64(59)
+        return out
+
+    def phase(self, lwe: np.ndarray, key=None) -> np.ndarray:
+        s = self.s_big if key is None else key
+        a = np.ascontiguousarray(lwe.reshape(-1, len(s) + 1), dtype=np.uint64)
+        out = np.zeros(a.shape[0], dtype=np.uint64)
+        lib().or_phase(len(s), ptr(np.ascontiguousarray(s, dtype=np.uint64)), ptr(a), a.shape[0], ptr(out))
+        return out
+
+    def decode16(self, lwe: np.ndarray) -> np.ndarray:
+        return np.array([lib().or_decode16(int(x)) for x in self.phase(lwe)], dtype=np.uint32)
+
+    def decrypt_radix(self, blocks: np.ndarray) -> int:
+        """RadixClientKey::decrypt: sum (block msg mod 4) * 4^i."""
+        d = self.decode16(blocks.reshape(-1, self.big + 1))
+        return int(sum(int(v % 4) << (2 * i) for i, v in enumerate(d))) & 0xFF
+
+    # -- server side
+    def keyswitch(self, lwe: np.ndarray) -> np.ndarray:
+        a = np.ascontiguousarray(lwe.reshape(-1, self.big + 1), dtype=np.uint64)
+        out = np.zeros((a.shape[0], self.n + 1), dtype=np.uint64)
+        lib().or_keyswitch(C.byref(self.P), ptr(self.ksk), ptr(a), a.shape[0], ptr(out))
+        return out
+
+    def blind_rotate(self, ks_lwe: np.ndarray, lut) -> np.ndarray:
+        l = (C.c_uint8 * 16)(*lut)
+        out = np.zeros(self.big + 1, dtype=np.uint64)
+        a = np.ascontiguousarray(ks_lwe, dtype=np.uint64)
+        lib().or_blind_rotate(self._pk, ptr(a), l, ptr(out))
+        return out
+
+    def gates(self, gates, slots: np.ndarray) -> np.ndarray:
+        """gates: list of (inputs [(slot, weight)], offset, lut[16])."""
+        arr = (Gate * len(gates))()
+        for q, (ins, off, lut) in enumerate(gates):
+            g = arr[q]
+            g.n_in = len(ins)
+            g.offset = off
+            for t, (i, w) in enumerate(ins):
+                g.in_idx[t] = i
+                g.in_w[t] = w
+            for t in range(16):
+                g.lut[t] = lut[t]
+        s = np.ascontiguousarray(slots.reshape(-1, self.big + 1), dtype=np.uint64)
+        out = np.zeros((len(gates), self.big + 1), dtype=np.uint64)
+        lib().or_gates(self._pk, ptr(self.ksk), arr, len(gates), ptr(s), ptr(out))
+        return out
+
+
+def load_fixture_key(path: str | None = None) -> dict:
+    if path is None:
+        path = os.path.join(os.path.dirname(HERE), "tests", "golden", "client_key")
+    with open(path, "rb") as f:
+        return parse_client_key(f.read())

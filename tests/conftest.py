@@ -1,0 +1,35 @@
+import os
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (os.path.join(REPO, "fhe-regex_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(REPO, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device 0)")
+    config.addinivalue_line("markers", "slow: long-running CPU test")
+
+
+@pytest.fixture(scope="session")
+def key_blob():
+    with open(os.path.join(GOLDEN, "client_key"), "rb") as f:
+        return f.read()
+
+
+@pytest.fixture(scope="session")
+def fixture_key():
+    import oracle_ffi
+    return oracle_ffi.load_fixture_key(os.path.join(GOLDEN, "client_key"))
+
+
+@pytest.fixture(scope="session")
+def oracle_k1(fixture_key):
+    """Oracle keys (k=1, N=2048) for server-key seed 42."""
+    import oracle_ffi
+    return oracle_ffi.Oracle(fixture_key, seed=42)

@@ -1,0 +1,267 @@
+"""GPU parity tests (MI355X): every kernel stage bit-exact against the CPU
+oracle on the same keys and inputs; decrypted match results equal to the
+reference's (plaintext oracle + the reference's own 25 vectors)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import fheregex as F
+import oracle_ffi as of
+import regex_oracle as ro
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+SEED = 42
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="module")
+def gctx(key_blob):
+    ctx = F.Context(device=0)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    return ctx
+
+
+def test_device_info(gctx):
+    assert "gfx950" in gctx.info()
+
+
+def test_ring_mul_bit_exact(gctx):
+    rng = np.random.default_rng(1)
+    P = of.P_GOLDILOCKS
+    a = rng.integers(0, P, (3, 2048), dtype=np.uint64)
+    b = rng.integers(0, P, (3, 2048), dtype=np.uint64)
+    b[1] = 0
+    b[1][5] = 1  # X^5
+    b[2] = rng.integers(-(1 << 22), 1 << 22, 2048) % P  # digit-sized operand
+    got = gctx.dev_ring_mul(a, b)
+    for i in range(3):
+        exp = np.zeros(2048, np.uint64)
+        of.lib().or_ring_mul(2048, of.ptr(np.ascontiguousarray(a[i])), of.ptr(np.ascontiguousarray(b[i])), of.ptr(exp))
+        assert (got[i] == exp).all(), i
+
+
+def test_keyswitch_bit_exact(gctx, oracle_k1):
+    O = oracle_k1
+    blocks = O.encrypt_blocks([3, 7, 0, 15, 9, 1, 2, 12, 4, 5, 6, 8, 10, 11, 13, 14, 3, 3, 3, 3, 0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13],
+                              seed=77)
+    got = gctx.dev_keyswitch(blocks)
+    exp = O.keyswitch(blocks)
+    assert got.shape == exp.shape
+    assert (got == exp).all()
+
+
+def test_blind_rotate_bit_exact(gctx, oracle_k1):
+    O = oracle_k1
+    blocks = O.encrypt_blocks([5, 12, 0], seed=31)
+    ks = O.keyswitch(blocks)
+    luts = [[(3 * m + 1) % 16 for m in range(16)], [int(m >= 4) for m in range(16)], [m ^ 5 for m in range(16)]]
+    got = gctx.dev_blind_rotate(ks, luts)
+    for i in range(3):
+        exp = O.blind_rotate(ks[i], luts[i])
+        assert (got[i] == exp).all(), i
+        assert O.decode16(got[i])[0] == luts[i][[5, 12, 0][i]]
+
+
+def test_gate_program_bit_exact(gctx, oracle_k1):
+    """Lincomb + KS + BR through fr_run_gates vs the oracle's gate evaluation."""
+    O = oracle_k1
+    s = b"Hi!"
+    ct = O.encrypt_str(s, seed=3)
+    hs = gctx.upload_radix(ct)
+    luts = [[int(v == (0x48 & 15)) for v in range(16)], [int(v == (0x69 >> 4)) for v in range(16)]]
+    gates = []
+    for j, (h, half) in enumerate([(hs[0], 0), (hs[1], 1)]):
+        g = F.Gate()
+        g.n_in = 2
+        g.offset = 0
+        g.in_[0], g.in_block[0], g.in_w[0] = h, 2 * half, 1
+        g.in_[1], g.in_block[1], g.in_w[1] = h, 2 * half + 1, 4
+        for v in range(16):
+            g.lut[v] = luts[j][v]
+        gates.append(g)
+    g = F.Gate()  # depends on both: [a + b == 2]
+    g.n_in = 2
+    g.in_[0], g.in_w[0] = 0x80000000 | 0, 1
+    g.in_[1], g.in_w[1] = 0x80000000 | 1, 1
+    for v in range(16):
+        g.lut[v] = int(v == 2)
+    gates.append(g)
+    outs = gctx.run_gates(gates)
+    got = np.stack([gctx.download_radix(o)[0] for o in outs])
+    slots = ct.reshape(-1, ct.shape[-1])
+    exp01 = O.gates([([(0, 1), (1, 4)], 0, luts[0]), ([(4 + 2, 1), (4 + 3, 4)], 0, luts[1])], slots)
+    assert (got[0] == exp01[0]).all() and (got[1] == exp01[1]).all()
+    exp2 = O.gates([([(0, 1), (1, 1)], 0, [int(v == 2) for v in range(16)])], exp01)
+    assert (got[2] == exp2[0]).all()
+    assert [int(O.decode16(got[i])[0]) for i in range(3)] == [1, 1, 1]
+
+
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_reference_vectors_trivial_content(gctx, v):
+    """src/regex/engine.rs:256-291 exactly as the reference runs them: trivial radix content."""
+    hs = [gctx.trivial(b) for b in v["content"].encode()]
+    out, st = gctx.has_match(hs, v["pattern"])
+    assert gctx.decrypt_radix(gctx.download_radix(out)) == v["expected"]
+    assert (st.ct_ops, st.cache_hits) == (v["ct_ops"], v["cache_hits"])
+
+
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_reference_vectors_encrypted_content(gctx, v):
+    hs = gctx.upload_radix(gctx.encrypt_str(v["content"], seed=len(v["content"]) + 100))
+    out, st = gctx.has_match(hs, v["pattern"])
+    assert gctx.decrypt_radix(gctx.download_radix(out)) == v["expected"]
+    for h in hs:
+        gctx.release(h)
+
+
+def test_eager_ops(gctx):
+    s = "aMz~ 0"
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=9))
+    dec = lambda h: gctx.decrypt_radix(gctx.download_radix(h))
+    for h, ch in zip(hs, s.encode()):
+        for c in (ch, ch - 1, ch + 1, ord("a"), ord("M")):
+            c &= 0xFF
+            assert dec(gctx.eq_const(h, c)) == int(ch == c)
+            assert dec(gctx.gt_const(h, c)) == int(ch > c)
+            assert dec(gctx.le_const(h, c)) == int(ch <= c)
+    e1, e0 = gctx.eq_const(hs[0], ord("a")), gctx.eq_const(hs[0], ord("b"))
+    assert [dec(gctx.and_(x, y)) for x, y in [(e1, e1), (e1, e0), (e0, e0)]] == [1, 0, 0]
+    assert [dec(gctx.or_(x, y)) for x, y in [(e1, e1), (e1, e0), (e0, e0)]] == [1, 1, 0]
+    assert [dec(gctx.not_(x)) for x in (e1, e0)] == [0, 1]
+    assert dec(gctx.not_(gctx.not_(e1))) == 1
+    # general radix bitand / bitor / bitxor-1 on characters
+    assert dec(gctx.and_(hs[0], hs[1])) == (ord("a") & ord("M"))
+    assert dec(gctx.or_(hs[0], hs[1])) == (ord("a") | ord("M"))
+    assert dec(gctx.not_(hs[2])) == (ord("z") ^ 1)
+    assert dec(gctx.or_many([e0, e0, e1, e0])) == 1
+    assert dec(gctx.or_many([e0] * 20)) == 0
+
+
+def _config(gctx, content, pattern, seed):
+    hs = gctx.upload_radix(gctx.encrypt_str(content, seed=seed))
+    out, st = gctx.has_match(hs, pattern)
+    got = gctx.decrypt_radix(gctx.download_radix(out))
+    for h in hs:
+        gctx.release(h)
+    return got, st
+
+
+def _printable(rng, n):
+    return "".join(chr(c) for c in rng.integers(0x20, 0x7F, n))
+
+
+def test_config1(gctx):
+    got, st = _config(gctx, "abc", "/^abc$/", 1)
+    assert got == 1 and (st.ct_ops, st.cache_hits) == (5, 0)
+
+
+@pytest.mark.parametrize("planted", [True, False])
+def test_config2_abc_64(gctx, planted):
+    rng = np.random.default_rng(2)
+    s = _printable(rng, 64)
+    if planted:
+        s = s[:17] + "abc" + s[20:]
+    exp = ro.has_match(s, "/abc/")
+    got, st = _config(gctx, s, "/abc/", 2)
+    assert got == exp.result and st.ct_ops == exp.ct_ops == 371
+
+
+def test_metric_abc_256(gctx):
+    rng = np.random.default_rng(0)
+    s = _printable(rng, 256)
+    s = s[:200] + "abc" + s[203:]
+    got, st = _config(gctx, s, "/abc/", 3)
+    assert got == 1 and st.ct_ops == 1523
+
+
+@pytest.mark.parametrize("kind", ["letters", "digit"])
+def test_config3_proxy(gctx, kind):
+    rng = np.random.default_rng(4)
+    s = "".join(chr(c) for c in rng.integers(ord("b"), ord("z") + 1, 256))
+    if kind == "digit":
+        s = s[:100] + "7" + s[101:]
+    exp = ro.has_match(s, "/^[a-z]+$/")
+    got, st = _config(gctx, s, "/^[a-z]+$/", 4)
+    assert got == exp.result == (1 if kind == "letters" else 0)
+
+
+def test_config3_as_written_is_a_parse_error(gctx):
+    hs = [gctx.trivial(ord("a"))]
+    with pytest.raises(F.ParseError):
+        gctx.has_match(hs, "/^[a-z0-9]+$/")
+
+
+def test_config4_the_i_1024(gctx):
+    rng = np.random.default_rng(5)
+    alpha = np.array(list(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ "))
+    s = bytes(rng.choice(alpha, 1024)).decode()
+    s = s.replace("the", "thx").replace("The", "Thx").replace("tHe", "tHx").replace("thE", "thx").replace("THE", "THX")
+    s = s.replace("tHE", "tHX").replace("ThE", "ThX").replace("THe", "THx")
+    exp0 = ro.has_match(s, "/the/i").result
+    got0, st = _config(gctx, s, "/the/i", 5)
+    assert got0 == exp0 == 0 and st.ct_ops == 12263
+    s1 = s[:700] + "ThE" + s[703:]
+    got1, _ = _config(gctx, s1, "/the/i", 6)
+    assert got1 == 1
+
+
+def test_config5_small(gctx):
+    pat = "/^a{2,8}(bc|de)+[^xyz]$/"
+    for s in ["aaabcdebcf", "aaabcdebcx", "abcf", "aadef"]:
+        exp = ro.has_match(s, pat)
+        got, st = _config(gctx, s, pat, 7)
+        assert got == exp.result, s
+        assert (st.ct_ops, st.cache_hits) == (exp.ct_ops, exp.cache_hits)
+
+
+def test_faithful_lowering(gctx):
+    rng = np.random.default_rng(8)
+    s = _printable(rng, 64)
+    s = s[:10] + "abc" + s[13:]
+    gctx.set_lowering(F.LOWER_FAITHFUL)
+    try:
+        got, st = _config(gctx, s, "/abc/", 8)
+    finally:
+        gctx.set_lowering(F.LOWER_THRESHOLD)
+    assert got == 1 and st.pbs == 743
+
+
+def test_start_range_shards_or_to_full(gctx):
+    rng = np.random.default_rng(9)
+    s = _printable(rng, 96)
+    s = s[:60] + "abc" + s[63:]
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=10))
+    parts = []
+    for lo, hi in [(0, 32), (32, 64), (64, 96)]:
+        out, _ = gctx.has_match(hs, "/abc/", lo, hi)
+        parts.append(out)
+    dec = [gctx.decrypt_radix(gctx.download_radix(p)) for p in parts]
+    assert dec == [0, 1, 0]
+    assert gctx.decrypt_radix(gctx.download_radix(gctx.or_many(parts))) == 1
+
+
+def test_k2_n1024_params(key_blob, fixture_key):
+    """The N=1024 variant: the same 2048-bit key read as k=2 polynomials of 1024."""
+    params = F.default_params(k=2, N=1024)
+    ctx = F.Context(0, params)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    O = of.Oracle(fixture_key, seed=SEED, k=2, N=1024)
+    ksk, bsk = ctx.export_server_key()
+    assert (ksk == O.ksk).all() and (bsk == O.bsk).all()
+    blocks = O.encrypt_blocks([6, 1], seed=5)
+    ks = O.keyswitch(blocks)
+    lut = [(5 * m + 2) % 16 for m in range(16)]
+    got = ctx.dev_blind_rotate(ks[:1], [lut])
+    assert (got[0] == O.blind_rotate(ks[0], lut)).all()
+    got, st = _config(ctx, "xxabcx", "/abc/", 11)
+    assert got == 1

@@ -1,0 +1,165 @@
+"""Product host logic through the C-ABI (no GPU): exports, parser, engine,
+lowering, keygen and the host/device scalar maps, checked against the oracle."""
+import ctypes
+import json
+import os
+import random
+
+import numpy as np
+import pytest
+
+import fheregex as F
+import oracle_ffi as of
+import regex_fuzz as rf
+import regex_oracle as ro
+from conftest import GOLDEN
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def test_library_exports_every_header_symbol():
+    lib = ctypes.CDLL(F.LIB_PATH)
+    syms = F.header_symbols()
+    assert len(syms) >= 35
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) <= set(F._SIGS)
+
+
+def test_host_only_context_fails_loudly_on_gpu_ops(key_blob):
+    ctx = F.Context(device=-1)
+    ctx.load_client_key(key_blob)
+    with pytest.raises(F.NoDevice):
+        ctx.upload_radix(np.zeros((1, 4, ctx.lwe_len), dtype=np.uint64))
+    with pytest.raises(F.NoDevice):
+        ctx.dev_ring_mul(np.zeros(2048, np.uint64), np.zeros(2048, np.uint64))
+
+
+@pytest.mark.parametrize("v", load("parser_vectors.json"), ids=lambda v: v["pattern"])
+def test_parser_golden(v):
+    assert F.parse(v["pattern"]) == v["ast"]
+
+
+@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD])
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_engine_golden(v, mode):
+    r = F.plain_match(v["content"], v["pattern"], mode)
+    assert (r.result_recorded, r.result_lowered, r.ct_ops, r.cache_hits) == (v["expected"], v["expected"], v["ct_ops"], v["cache_hits"])
+
+
+@pytest.mark.parametrize("pattern,exc", [("/a{}/", F.ReferencePanic), ("/ab", F.ParseError), ("/[a-z0-9]/", F.ParseError),
+                                         ("/^[a-z0-9]+$/", F.ParseError), ("/a+?/", F.ParseError), ("/a/x", F.ParseError),
+                                         ("/a{99999999999999999999}/", F.ReferencePanic)])
+def test_parse_errors_match_reference(pattern, exc):
+    with pytest.raises(exc):
+        F.parse(pattern)
+
+
+def test_empty_seq_panics_like_reference():
+    with pytest.raises(F.ReferencePanic):
+        F.plain_match("a", "/^/")
+    assert F.plain_match("", "/^/").result_recorded == 0
+
+
+def test_fuzz_vs_oracle():
+    rng = random.Random(7)
+    n = 0
+    while n < 400:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(0, 6))
+        try:
+            exp = ro.has_match(c, p)
+            e_exc = None
+        except (ro.ParseError, ro.ReferencePanic) as e:
+            exp, e_exc = None, type(e).__name__
+        if exp is not None and exp.n_branches > 500:
+            continue
+        for mode in (F.LOWER_FAITHFUL, F.LOWER_THRESHOLD):
+            try:
+                r = F.plain_match(c, p, mode)
+                got, g_exc = (r.result_recorded, r.result_lowered, r.ct_ops, r.cache_hits), None
+            except (F.ParseError, F.ReferencePanic) as e:
+                got, g_exc = None, type(e).__name__
+            if e_exc or g_exc:
+                assert e_exc == g_exc, (c, p)
+            else:
+                assert got == (exp.result, exp.result, exp.ct_ops, exp.cache_hits), (c, p, mode)
+        n += 1
+
+
+def test_config_counts_and_pbs():
+    # reference ct_ops and the faithful build's PBS counts
+    cases = [("abc", "/^abc$/", 5, 11), ("x" * 64, "/abc/", 371, 743), ("x" * 256, "/abc/", 1523, 3047),
+             ("b" * 256, "/^[a-z]+$/", 1023, 2047), ("x" * 1024, "/the/i", 12263, 24527)]
+    for c, p, ops, pbs in cases:
+        r = F.plain_match(c, p, F.LOWER_FAITHFUL)
+        assert (r.ct_ops, r.cache_hits, r.pbs) == (ops, 0, pbs), p
+        t = F.plain_match(c, p, F.LOWER_THRESHOLD)
+        assert t.ct_ops == ops and t.pbs < pbs and t.levels <= 6, (p, t.pbs, t.levels)
+
+
+@pytest.mark.parametrize("content,pattern", [("q" * 100 + "abc" + "q" * 40, "/abc/"), ("b" * 90 + "z", "/^[a-z]+$/"),
+                                             ("aaa" + "bcde" * 3 + "f", "/^a{2,8}(bc|de)+[^xyz]$/"),
+                                             ("xx The end", "/the/i"), ("a" * 50 + "0", "/^[a-z]+$/")])
+def test_large_plain_vs_oracle(content, pattern):
+    exp = ro.has_match(content, pattern)
+    r = F.plain_match(content, pattern)
+    assert (r.result_recorded, r.result_lowered, r.ct_ops, r.cache_hits) == (exp.result, exp.result, exp.ct_ops, exp.cache_hits)
+
+
+def test_start_range_partition_is_or():
+    rng = random.Random(3)
+    for _ in range(50):
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, 9)
+        try:
+            full = F.plain_match(c, p).result_lowered
+        except (F.ParseError, F.ReferencePanic):
+            continue
+        cut = rng.randint(0, len(c))
+        a = F.plain_match(c, p, start_lo=0, start_hi=cut).result_lowered
+        b = F.plain_match(c, p, start_lo=cut, start_hi=len(c)).result_lowered
+        assert full == (a | b), (c, p, cut)
+
+
+def test_scalar_maps_match_oracle():
+    L, O = F.lib(), of.lib()
+    P = of.P_GOLDILOCKS
+    rng = np.random.default_rng(9)
+    xs = [0, 1, 2, P - 1, P - 2, (1 << 63), (1 << 41) - (1 << 9), (1 << 40) - (1 << 8), P - ((1 << 40) - (1 << 8))]
+    xs += [int(v) for v in rng.integers(0, P, 5000, dtype=np.uint64)]
+    for x in xs:
+        y = int(rng.integers(0, P, dtype=np.uint64))
+        assert L.fr_debug_scalar(0, x, y) == O.or_gl_mul(x, y)
+        assert L.fr_debug_scalar(1, x, 0) == O.or_decompose_pbs(x)
+        assert L.fr_debug_scalar(2, x, 0) == O.or_conv(x)
+    dig = (ctypes.c_int32 * 5)()
+    for x in [int(v) for v in rng.integers(0, 2**64 - 1, 3000, dtype=np.uint64)] + [0, 2**64 - 1, 2**48, 2**63]:
+        assert L.fr_debug_scalar(3, x, 12) == O.or_mod_switch(x, 12)
+        O.or_ks_decompose(x, 3, 5, dig)
+        for j in range(5):
+            assert L.fr_debug_scalar(4, x, j) == (dig[j] & 0xFFFFFFFFFFFFFFFF)
+
+
+def test_keygen_matches_oracle(key_blob, oracle_k1):
+    ctx = F.Context(device=-1)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(42)
+    ksk, bsk = ctx.export_server_key()
+    assert ksk.shape == oracle_k1.ksk.shape and bsk.shape == oracle_k1.bsk.shape
+    assert (ksk == oracle_k1.ksk).all()
+    assert (bsk == oracle_k1.bsk).all()
+
+
+def test_product_encrypt_matches_oracle(key_blob, oracle_k1):
+    ctx = F.Context(device=-1)
+    ctx.load_client_key(key_blob)
+    a = ctx.encrypt_str("abc~", seed=5)
+    b = oracle_k1.encrypt_str(b"abc~", seed=5)
+    assert (a == b).all()
+    assert [ctx.decrypt_radix(a[i]) for i in range(4)] == list(b"abc~")
+    with pytest.raises(ValueError):
+        ctx.encrypt_str("caf\xe9", seed=1)

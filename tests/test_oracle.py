@@ -1,0 +1,127 @@
+"""The oracle itself, pinned against the reference's own vectors and fixture."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import oracle_ffi as of
+import regex_oracle as ro
+from conftest import GOLDEN
+
+
+def load(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("v", load("parser_vectors.json"), ids=lambda v: v["pattern"])
+def test_oracle_parser_golden(v):
+    # src/regex/parser.rs:358-678
+    assert str(ro.parse(v["pattern"])) == v["ast"]
+
+
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_oracle_engine_golden(v):
+    # src/regex/engine.rs:256-280 results; SURVEY App. B counts
+    r = ro.has_match(v["content"], v["pattern"])
+    assert (r.result, r.ct_ops, r.cache_hits) == (v["expected"], v["ct_ops"], v["cache_hits"])
+
+
+@pytest.mark.parametrize("pattern,err", [("/a{}/", ro.ReferencePanic), ("/ab", ro.ParseError), ("/[a-z0-9]/", ro.ParseError),
+                                         ("/^[a-z0-9]+$/", ro.ParseError), ("/a+?/", ro.ParseError), ("/1/", ro.ParseError),
+                                         ("/a/x", ro.ParseError), ("/[]/", ro.ParseError), ("/(a/", ro.ParseError)])
+def test_oracle_parse_errors(pattern, err):
+    with pytest.raises(err):
+        ro.parse(pattern)
+
+
+def test_oracle_empty_seq_panics():
+    assert str(ro.parse("/^/")) == "Seq(SOF,Seq())"
+    with pytest.raises(ro.ReferencePanic):
+        ro.has_match("a", "/^/")
+    assert ro.has_match("", "/^/").result == 0  # p >= L short-circuits before the panic
+
+
+def test_config_counts():
+    # SURVEY §8(a) op-count table (reference-faithful)
+    assert (lambda r: (r.ct_ops, r.cache_hits))(ro.has_match("abc", "/^abc$/")) == (5, 0)
+    assert ro.has_match("x" * 64, "/abc/").ct_ops == 371
+    assert ro.has_match("x" * 256, "/abc/").ct_ops == 1523
+    assert ro.has_match("b" * 256, "/^[a-z]+$/").ct_ops == 1023
+
+
+def test_fixture_key_layout(fixture_key):
+    k = fixture_key
+    assert (k["n"], k["k"], k["N"]) == (742, 1, 2048)
+    assert (k["pbs_base_log"], k["pbs_level"], k["ks_base_log"], k["ks_level"]) == (23, 1, 3, 5)
+    assert (k["message_modulus"], k["carry_modulus"], k["num_blocks"]) == (4, 4, 4)
+    assert int(k["s_big"].sum()) == 1031 and int(k["s_small"].sum()) == 395
+    assert (k["glwe"] == k["s_big"]).all()
+
+
+def test_ring_mul_vs_schoolbook():
+    L = of.lib()
+    rng = np.random.default_rng(3)
+    for N in (16, 256):
+        a = rng.integers(0, of.P_GOLDILOCKS, N, dtype=np.uint64)
+        b = rng.integers(0, of.P_GOLDILOCKS, N, dtype=np.uint64)
+        o1 = np.zeros(N, np.uint64)
+        o2 = np.zeros(N, np.uint64)
+        L.or_ring_mul(N, of.ptr(a), of.ptr(b), of.ptr(o1))
+        L.or_ring_mul_schoolbook(N, of.ptr(a), of.ptr(b), of.ptr(o2))
+        assert (o1 == o2).all()
+    # pure-python negacyclic product for a tiny case
+    N, P = 8, of.P_GOLDILOCKS
+    a = rng.integers(0, P, N, dtype=np.uint64)
+    b = rng.integers(0, P, N, dtype=np.uint64)
+    ref = [0] * N
+    for i in range(N):
+        for j in range(N):
+            m = int(a[i]) * int(b[j]) % P
+            if i + j < N:
+                ref[i + j] = (ref[i + j] + m) % P
+            else:
+                ref[i + j - N] = (ref[i + j - N] - m) % P
+    o = np.zeros(N, np.uint64)
+    L.or_ring_mul_schoolbook(N, of.ptr(a), of.ptr(b), of.ptr(o))
+    assert [int(x) for x in o] == ref
+
+
+def test_decompose_and_conv_properties():
+    L = of.lib()
+    P = of.P_GOLDILOCKS
+    g = (1 << 41) - (1 << 9)
+    rng = np.random.default_rng(5)
+    xs = [0, 1, g // 2, g // 2 + 1, P - 1, P - 2, P - g // 2, (1 << 63), P // 2] + [int(x) for x in rng.integers(0, P, 2000, dtype=np.uint64)]
+    for x in xs:
+        d = L.or_decompose_pbs(x)
+        ds = d if d < P // 2 else d - P
+        assert -(1 << 22) <= ds < (1 << 22)
+        err = (x - ds * g) % P
+        err = err if err < P // 2 else err - P
+        assert abs(err) <= g // 2 + 1
+        y = L.or_conv(x)
+        assert y == ((x << 64) + (P - 1) // 2) // P & (2**64 - 1)
+
+
+def test_encrypt_decrypt_roundtrip(oracle_k1):
+    ct = oracle_k1.encrypt_str(b"Hello, World~", seed=11)
+    assert bytes(oracle_k1.decrypt_radix(ct[i]) for i in range(ct.shape[0])) == b"Hello, World~"
+    t = oracle_k1.trivial_blocks([1, 2, 3, 0])
+    assert oracle_k1.decrypt_radix(t) == 1 + 2 * 4 + 3 * 16
+
+
+def test_oracle_pbs_lut(oracle_k1):
+    """KS -> BR -> SE on fresh and trivial inputs decrypts to the LUT value."""
+    O = oracle_k1
+    msgs = [0, 5, 15, 9]
+    blocks = O.encrypt_blocks(msgs, seed=21)
+    blocks[3] = O.trivial_blocks([9])[0]
+    luts = [[(3 * m + 1) % 16 for m in range(16)], [m ^ 1 for m in range(16)], list(range(16)), [1] * 16]
+    gates = [([(i, 1)], 0, luts[i]) for i in range(4)]
+    out = O.gates(gates, blocks)
+    dec = O.decode16(out)
+    assert [int(d) for d in dec] == [luts[i][msgs[i]] for i in range(4)]
+    # trivial input: bootstrapping a trivial ciphertext yields a trivial (noiseless) one
+    assert (out[3][:-1] == 0).all()
