@@ -41,7 +41,7 @@ def test_ring_mul_bit_exact(gctx):
     b = rng.integers(0, P, (3, 2048), dtype=np.uint64)
     b[1] = 0
     b[1][5] = 1  # X^5
-    b[2] = rng.integers(-(1 << 22), 1 << 22, 2048) % P  # digit-sized operand
+    b[2] = np.array([int(d) % P for d in rng.integers(-(1 << 22), 1 << 22, 2048)], dtype=np.uint64)  # digit-sized
     got = gctx.dev_ring_mul(a, b)
     for i in range(3):
         exp = np.zeros(2048, np.uint64)
@@ -202,7 +202,7 @@ def test_config3_as_written_is_a_parse_error(gctx):
 
 def test_config4_the_i_1024(gctx):
     rng = np.random.default_rng(5)
-    alpha = np.array(list(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ "))
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
     s = bytes(rng.choice(alpha, 1024)).decode()
     s = s.replace("the", "thx").replace("The", "Thx").replace("tHe", "tHx").replace("thE", "thx").replace("THE", "THX")
     s = s.replace("tHE", "tHX").replace("ThE", "ThX").replace("THe", "THx")
