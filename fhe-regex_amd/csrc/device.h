@@ -72,6 +72,7 @@ class Device {
 
     Params p_;
     int dev_;
+    int e_ = 8;   // coefficients per lane in the NTT kernels (8 or 16)
     void* stream_ = nullptr;  // hipStream_t
     uint64_t* d_ksk_ = nullptr;
     uint64_t* d_bsk_ = nullptr;  // NTT domain, scaled by 1/N

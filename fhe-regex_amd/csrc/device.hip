@@ -19,11 +19,15 @@
 // transform: zeta[k] = psi^brv(k); outputs in bit-reversed slot order.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
+#include <cstdlib>
+#include <type_traits>
 #include <cstring>
 #include <sstream>
 
 #include "device.h"
+#include "gl_device.h"
 #include "keys.h"
 
 namespace fr {
@@ -37,198 +41,160 @@ namespace fr {
     } while (0)
 
 // ------------------------------------------------------------------ geometry
-template <int N>
-struct Geom {
-    static constexpr int LOG = (N == 2048) ? 11 : (N == 1024) ? 10 : (N == 512) ? 9 : 0;
-    static_assert(LOG >= 9, "N must be 512, 1024 or 2048");
-    static constexpr int T = N / 16;   // lanes per polynomial
-    static constexpr int R = N / 256;  // phase-2 lane stride
+constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
+
+// N-point negacyclic NTT spread over T = N/E lanes holding E coefficients
+// each.  The LOG = log2 N stages run as NPH register-resident phases of e =
+// log2 E stages; phase p's lane owns the E elements that differ in index bits
+// [lo(p), lo(p)+e), and two consecutive phases are joined by one LDS
+// exchange.  Forward stage s pairs bit LOG-1-s with zeta[(1<<s) + (j >> (LOG-s))],
+// zeta[k] = psi^brv(k); the inverse uses psi^-brv(k) = -zeta[3*2^s - 1 - k].
+template <int N, int E>
+struct NttGeo {
+    static constexpr int LOG = ilog2c(N);
+    static constexpr int e = ilog2c(E);
+    static constexpr int T = N / E;
+    static constexpr int NPH = (LOG + e - 1) / e;
     static constexpr int NP = N + N / 16;  // padded LDS row (u64)
+    static_assert((1 << LOG) == N && (1 << e) == E, "powers of two");
+    static constexpr int lo(int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
+    static constexpr int s_begin(int p) { return p * e; }
+    static constexpr int s_end(int p) { return (p + 1) * e < LOG ? (p + 1) * e : LOG; }
     __device__ static __forceinline__ int pad(int i) { return i + (i >> 4); }
-    __device__ static __forceinline__ int idx1(int tl, int m) { return tl + T * m; }
-    __device__ static __forceinline__ int idx2(int tl, int m) { return (tl / R) * T + (tl % R) + R * m; }
-    __device__ static __forceinline__ int idx3(int tl, int m) { return 16 * tl + m; }
+    template <int p>
+    __device__ static __forceinline__ int idx(int tl, int m) {
+        constexpr int L = lo(p);
+        return ((tl >> L) << (L + e)) | (m << L) | (tl & ((1 << L) - 1));
+    }
 };
 
-__device__ __forceinline__ void ct_bf(uint64_t& x, uint64_t& y, uint64_t z) {
-    uint64_t t = gl_mul(z, y);
-    y = gl_sub(x, t);
-    x = gl_add(x, t);
-}
-__device__ __forceinline__ void gs_bf(uint64_t& x, uint64_t& y, uint64_t z) {
-    uint64_t u = x, v = y;
-    x = gl_add(u, v);
-    y = gl_mul(gl_sub(u, v), z);
-}
-
-// ----- forward phases (stage s: distance N >> (s+1); zeta index (1<<s) + (j >> (LOG-s)))
-template <int N>
-__device__ __forceinline__ void fwd_phase1(uint64_t (&x)[16], const uint64_t* zt) {
+template <int N, int E, int p>
+__device__ __forceinline__ void fwd_phase(uint64_t (&x)[E], const uint64_t* zt, int tl) {
+    using G = NttGeo<N, E>;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int d = 8 >> q;
+    for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = zt[(1 << q) + (m >> (4 - q))];
-            ct_bf(x[m], x[m + d], z);
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            const int j = G::template idx<p>(tl, m);
+            gd::ct(x[m], x[m + dm], zt[(1 << s) + (j >> (G::LOG - s))]);
         }
     }
 }
-template <int N>
-__device__ __forceinline__ void fwd_phase2(uint64_t (&x)[16], const uint64_t* zt, int tl) {
-    using G = Geom<N>;
-    const int c = tl / G::R;
+template <int N, int E, int p>
+__device__ __forceinline__ void inv_phase(uint64_t (&x)[E], const uint64_t* zt, int tl) {
+    using G = NttGeo<N, E>;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        const int s = 4 + q, d = 8 >> q;
+    for (int s = G::s_end(p) - 1; s >= G::s_begin(p); --s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = zt[(1 << s) + (c << q) + (m >> (4 - q))];
-            ct_bf(x[m], x[m + d], z);
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            const int j = G::template idx<p>(tl, m);
+            const int k = (1 << s) + (j >> (G::LOG - s));
+            gd::gs(x[m], x[m + dm], zt[3 * (1 << s) - 1 - k]);
         }
     }
 }
-template <int N>
-__device__ __forceinline__ void fwd_phase3(uint64_t (&x)[16], const uint64_t* zt, int tl) {
-    using G = Geom<N>;
-#pragma unroll
-    for (int s = 8; s < G::LOG; ++s) {
-        const int d = N >> (s + 1);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = zt[(1 << s) + ((16 * tl + m) >> (G::LOG - s))];
-            ct_bf(x[m], x[m + d], z);
-        }
-    }
-}
-// ----- inverse phases (reverse order, GS butterflies with izeta)
-template <int N>
-__device__ __forceinline__ void inv_phase3(uint64_t (&x)[16], const uint64_t* izt, int tl) {
-    using G = Geom<N>;
-#pragma unroll
-    for (int s = G::LOG - 1; s >= 8; --s) {
-        const int d = N >> (s + 1);
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = izt[(1 << s) + ((16 * tl + m) >> (G::LOG - s))];
-            gs_bf(x[m], x[m + d], z);
-        }
-    }
-}
-template <int N>
-__device__ __forceinline__ void inv_phase2(uint64_t (&x)[16], const uint64_t* izt, int tl) {
-    using G = Geom<N>;
-    const int c = tl / G::R;
-#pragma unroll
-    for (int q = 3; q >= 0; --q) {
-        const int s = 4 + q, d = 8 >> q;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = izt[(1 << s) + (c << q) + (m >> (4 - q))];
-            gs_bf(x[m], x[m + d], z);
-        }
-    }
-}
-template <int N>
-__device__ __forceinline__ void inv_phase1(uint64_t (&x)[16], const uint64_t* izt) {
-#pragma unroll
-    for (int q = 3; q >= 0; --q) {
-        const int d = 8 >> q;
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            if (m & d) continue;
-            const uint64_t z = izt[(1 << q) + (m >> (4 - q))];
-            gs_bf(x[m], x[m + d], z);
-        }
-    }
-}
-
-// LDS exchange between lane layouts (row = this lane's polynomial)
-template <int N, int FROM, int TO>
-__device__ __forceinline__ void exchange(uint64_t (&x)[16], uint64_t* row, int tl) {
-    using G = Geom<N>;
+// LDS exchange between the layouts of phases PF and PT (row = this lane's polynomial)
+template <int N, int E, int PF, int PT>
+__device__ __forceinline__ void exchange(uint64_t (&x)[E], uint64_t* row, int tl) {
+    using G = NttGeo<N, E>;
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        int i = FROM == 1 ? G::idx1(tl, m) : FROM == 2 ? G::idx2(tl, m) : G::idx3(tl, m);
-        row[G::pad(i)] = x[m];
-    }
+    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<PF>(tl, m))] = x[m];
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        int i = TO == 1 ? G::idx1(tl, m) : TO == 2 ? G::idx2(tl, m) : G::idx3(tl, m);
-        x[m] = row[G::pad(i)];
-    }
+    for (int m = 0; m < E; ++m) x[m] = row[G::pad(G::template idx<PT>(tl, m))];
 }
 
-template <int N>
-__device__ __forceinline__ void forward_ntt(uint64_t (&x)[16], uint64_t* row, const uint64_t* zt, int tl) {
-    fwd_phase1<N>(x, zt);
-    exchange<N, 1, 2>(x, row, tl);
-    fwd_phase2<N>(x, zt, tl);
-    exchange<N, 2, 3>(x, row, tl);
-    fwd_phase3<N>(x, zt, tl);
+template <int N, int E, int p>
+__device__ __forceinline__ void forward_from(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
+    fwd_phase<N, E, p>(x, zt, tl);
+    if constexpr (p + 1 < NttGeo<N, E>::NPH) {
+        exchange<N, E, p, p + 1>(x, row, tl);
+        forward_from<N, E, p + 1>(x, row, zt, tl);
+    }
 }
-template <int N>
-__device__ __forceinline__ void inverse_ntt(uint64_t (&x)[16], uint64_t* row, const uint64_t* izt, int tl) {
-    inv_phase3<N>(x, izt, tl);
-    exchange<N, 3, 2>(x, row, tl);
-    inv_phase2<N>(x, izt, tl);
-    exchange<N, 2, 1>(x, row, tl);
-    inv_phase1<N>(x, izt);
+template <int N, int E, int p>
+__device__ __forceinline__ void inverse_from(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
+    inv_phase<N, E, p>(x, zt, tl);
+    if constexpr (p > 0) {
+        exchange<N, E, p, p - 1>(x, row, tl);
+        inverse_from<N, E, p - 1>(x, row, zt, tl);
+    }
+}
+// natural order (phase-0 layout) -> bit-reversed slots (last-phase layout)
+template <int N, int E>
+__device__ __forceinline__ void forward_ntt(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
+    forward_from<N, E, 0>(x, row, zt, tl);
+}
+// last-phase layout -> natural order, without the 1/N factor
+template <int N, int E>
+__device__ __forceinline__ void inverse_ntt(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
+    inverse_from<N, E, NttGeo<N, E>::NPH - 1>(x, row, zt, tl);
 }
 
 // ------------------------------------------------------------ blind rotation
-template <int N, int K>
+template <int N, int K, int E>
 constexpr size_t br_smem_bytes() {
-    return sizeof(uint64_t) * ((size_t)(K + 1) * Geom<N>::NP + 2 * (size_t)N) + 16 + 2 * 1024;
+    return sizeof(uint64_t) * ((size_t)(K + 1) * NttGeo<N, E>::NP + (size_t)N) + 16 + 2 * 1024;
+}
+template <int N, int K, int E>
+constexpr int br_threads() {
+    return (K + 1) * (N / E);
 }
 
-template <int N, int K>
-__global__ void __launch_bounds__((K + 1) * (N / 16))
+// BSK slot layout for lane tl / register m of the last NTT phase: m*T + tl
+template <int N, int E>
+__device__ __forceinline__ int bsk_pos(int tl, int m) {
+    return m * NttGeo<N, E>::T + tl;
+}
+
+// minimum waves per SIMD: E=8 caps registers at 128 so two 512-thread
+// workgroups share a CU (measured +27% saturated throughput over 146 VGPRs)
+template <int E>
+constexpr int br_min_waves() {
+    return E == 8 ? 4 : 1;
+}
+template <int N, int K, int E>
+__global__ void __launch_bounds__((K + 1) * (N / E), br_min_waves<E>())
 k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
                const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ tw, uint64_t* __restrict__ arena,
                int slot_stride) {
-    using G = Geom<N>;
-    constexpr int NT = (K + 1) * G::T;
+    using G = NttGeo<N, E>;
+    constexpr int NT = br_threads<N, K, E>();
+    constexpr int LAST = G::NPH - 1;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    uint64_t* xbuf = smem;                       // (K+1) rows of NP
-    uint64_t* zt = xbuf + (K + 1) * G::NP;       // N
-    uint64_t* izt = zt + N;                      // N
-    uint8_t* lut = (uint8_t*)(izt + N);          // 16
-    uint16_t* abar = (uint16_t*)(lut + 16);      // n (<= 1024)
+    uint64_t* xbuf = smem;                   // (K+1) rows of NP
+    uint64_t* zt = xbuf + (K + 1) * G::NP;   // N
+    uint8_t* lut = (uint8_t*)(zt + N);       // 16
+    uint16_t* abar = (uint16_t*)(lut + 16);  // n (<= 1024)
 
     const int tid = threadIdx.x;
     const int P = tid / G::T, tl = tid % G::T;
     const int g = blockIdx.x;
     const uint64_t* in = ks + (size_t)g * ks_stride;
 
-    for (int i = tid; i < N; i += NT) {
-        zt[i] = tw[i];
-        izt[i] = tw[N + i];
-    }
+    for (int i = tid; i < N; i += NT) zt[i] = tw[i];
     if (tid < 16) lut[tid] = gates[g].lut[tid];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
     const uint32_t bbar = mod_switch(in[n], G::LOG + 1);
     __syncthreads();
 
     uint64_t* row = xbuf + P * G::NP;
-    uint64_t acc[16];
+    uint64_t acc[E];  // canonical, natural order: coefficient idx<0>(tl, m)
     {
         constexpr int box = N / 16, half = box / 2;
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
+        for (int m = 0; m < E; ++m) {
             acc[m] = 0;
             if (P == K) {
-                int s = (G::idx1(tl, m) + (int)bbar) & (2 * N - 1);
-                int sp = s < N ? s : s - N;
-                int mm = (sp + half) / box;
-                uint64_t v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
+                const int s = (G::template idx<0>(tl, m) + (int)bbar) & (2 * N - 1);
+                const int sp = s < N ? s : s - N;
+                const int mm = (sp + half) / box;
+                const uint64_t v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
                 acc[m] = s < N ? v : gl_neg(v);
             }
         }
@@ -239,49 +205,48 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         const int a = abar[i];
         if (a == 0) continue;  // X^0*acc - acc = 0: exact no-op (uniform branch)
         // 1. rotate (X^a - 1) * acc and decompose
-        uint64_t x[16];
+        uint64_t x[E];
         __syncthreads();
 #pragma unroll
-        for (int m = 0; m < 16; ++m) row[G::pad(G::idx1(tl, m))] = acc[m];
+        for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = acc[m];
         __syncthreads();
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            int s = (G::idx1(tl, m) - a) & (2 * N - 1);
-            uint64_t v = s < N ? row[G::pad(s)] : gl_neg(row[G::pad(s - N)]);
+        for (int m = 0; m < E; ++m) {
+            const int s = (G::template idx<0>(tl, m) - a) & (2 * N - 1);
+            const uint64_t v = s < N ? row[G::pad(s)] : gl_neg(row[G::pad(s - N)]);
             x[m] = pbs_decompose(gl_sub(v, acc[m]));
         }
         // 2. forward NTT of this lane group's digit polynomial
-        forward_ntt<N>(x, row, zt, tl);
-        // 3. external product MAC: out_P = sum_r D_r * GGSW_i[r][P]
+        forward_ntt<N, E>(x, row, zt, tl);
+        // 3. external product MAC (in place): x_P = sum_r D_r * GGSW_i[r][P]
         __syncthreads();
 #pragma unroll
-        for (int m = 0; m < 16; ++m) row[G::pad(G::idx3(tl, m))] = x[m];
+        for (int m = 0; m < E; ++m) row[G::pad(G::template idx<LAST>(tl, m))] = x[m];
         __syncthreads();
         const uint64_t* gi = bsk + (size_t)i * ggsw;
-        uint64_t y[16];
 #pragma unroll
-        for (int m = 0; m < 16; ++m) {
-            const int pos = G::pad(G::idx3(tl, m));
+        for (int m = 0; m < E; ++m) {
+            const int pos = G::pad(G::template idx<LAST>(tl, m));
             uint64_t sacc = 0;
 #pragma unroll
             for (int r = 0; r <= K; ++r) {
                 const uint64_t d = (r == P) ? x[m] : xbuf[r * G::NP + pos];
-                const uint64_t gv = gi[((size_t)(r * (K + 1) + P)) * N + m * G::T + tl];
-                sacc = gl_add(sacc, gl_mul(d, gv));
+                const uint64_t gv = gi[((size_t)(r * (K + 1) + P)) * N + bsk_pos<N, E>(tl, m)];
+                sacc = r == 0 ? gd::mul(d, gv) : gd::add_g(sacc, gd::mul(d, gv));
             }
-            y[m] = sacc;
+            x[m] = sacc;
         }
-        // 4. inverse NTT and accumulate
-        inverse_ntt<N>(y, row, izt, tl);
+        // 4. inverse NTT and accumulate (1/N is folded into the BSK)
+        inverse_ntt<N, E>(x, row, zt, tl);
 #pragma unroll
-        for (int m = 0; m < 16; ++m) acc[m] = gl_add(acc[m], y[m]);
+        for (int m = 0; m < E; ++m) acc[m] = gd::canon(gd::add_c(x[m], acc[m]));
     }
 
     // sample extract (coefficient 0) under the flattened key, then Z_p -> 2^64
     uint64_t* out = arena + (size_t)gates[g].out_slot * slot_stride;
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int j = G::idx1(tl, m);
+    for (int m = 0; m < E; ++m) {
+        const int j = G::template idx<0>(tl, m);
         if (P < K) {
             const int t = j == 0 ? 0 : N - j;
             const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
@@ -293,12 +258,12 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
 }
 
 // ------------------------------------------------------ BSK -> NTT domain
-template <int N, int K>
-__global__ void __launch_bounds__((K + 1) * (N / 16))
+template <int N, int K, int E>
+__global__ void __launch_bounds__((K + 1) * (N / E))
 k_bsk_to_ntt(const uint64_t* __restrict__ coef, const uint64_t* __restrict__ tw, uint64_t n_inv,
              uint64_t* __restrict__ out) {
-    using G = Geom<N>;
-    constexpr int NT = (K + 1) * G::T;
+    using G = NttGeo<N, E>;
+    constexpr int NT = br_threads<N, K, E>();
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* xbuf = smem;
     uint64_t* zt = xbuf + (K + 1) * G::NP;
@@ -306,69 +271,71 @@ k_bsk_to_ntt(const uint64_t* __restrict__ coef, const uint64_t* __restrict__ tw,
     for (int i = tid; i < N; i += NT) zt[i] = tw[i];
     __syncthreads();
     const size_t poly = ((size_t)blockIdx.x * (K + 1) + P) * N;  // blockIdx.x = i*(K+1) + r
-    uint64_t x[16];
+    uint64_t x[E];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) x[m] = coef[poly + G::idx1(tl, m)];
-    forward_ntt<N>(x, xbuf + P * G::NP, zt, tl);
+    for (int m = 0; m < E; ++m) x[m] = coef[poly + G::template idx<0>(tl, m)];
+    forward_ntt<N, E>(x, xbuf + P * G::NP, zt, tl);
 #pragma unroll
-    for (int m = 0; m < 16; ++m) out[poly + m * G::T + tl] = gl_mul(x[m], n_inv);
+    for (int m = 0; m < E; ++m) out[poly + bsk_pos<N, E>(tl, m)] = gl_mul(gd::canon(x[m]), n_inv);
 }
 
 // ------------------------------------------------ ring product (parity test)
-template <int N>
-__global__ void __launch_bounds__(2 * (N / 16))
+template <int N, int E>
+__global__ void __launch_bounds__(2 * (N / E))
 k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const uint64_t* __restrict__ tw,
            uint64_t n_inv, uint64_t* __restrict__ out) {
-    using G = Geom<N>;
+    using G = NttGeo<N, E>;
+    constexpr int LAST = G::NPH - 1;
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* xbuf = smem;
     uint64_t* zt = xbuf + 2 * G::NP;
-    uint64_t* izt = zt + N;
     const int tid = threadIdx.x, P = tid / G::T, tl = tid % G::T;
-    for (int i = tid; i < N; i += 2 * G::T) {
-        zt[i] = tw[i];
-        izt[i] = tw[N + i];
-    }
+    for (int i = tid; i < N; i += 2 * G::T) zt[i] = tw[i];
     __syncthreads();
     const uint64_t* src = (P == 0 ? a : b) + (size_t)blockIdx.x * N;
-    uint64_t x[16];
+    uint64_t x[E];
 #pragma unroll
-    for (int m = 0; m < 16; ++m) x[m] = src[G::idx1(tl, m)];
+    for (int m = 0; m < E; ++m) x[m] = src[G::template idx<0>(tl, m)];
     uint64_t* row = xbuf + P * G::NP;
-    forward_ntt<N>(x, row, zt, tl);
+    forward_ntt<N, E>(x, row, zt, tl);
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < 16; ++m) row[G::pad(G::idx3(tl, m))] = x[m];
+    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<LAST>(tl, m))] = x[m];
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < 16; ++m) {
-        const int pos = G::pad(G::idx3(tl, m));
-        x[m] = gl_mul(gl_mul(xbuf[pos], xbuf[G::NP + pos]), n_inv);
+    for (int m = 0; m < E; ++m) {
+        const int pos = G::pad(G::template idx<LAST>(tl, m));
+        x[m] = gd::mul(gd::mul(xbuf[pos], xbuf[G::NP + pos]), n_inv);
     }
-    inverse_ntt<N>(x, row, izt, tl);
+    inverse_ntt<N, E>(x, row, zt, tl);
     if (P == 0) {
 #pragma unroll
-        for (int m = 0; m < 16; ++m) out[(size_t)blockIdx.x * N + G::idx1(tl, m)] = x[m];
+        for (int m = 0; m < E; ++m) out[(size_t)blockIdx.x * N + G::template idx<0>(tl, m)] = gd::canon(x[m]);
     }
 }
 
 // ------------------------------------------------- lincomb + keyswitch
-// Tile: 32 gates x 64 output columns per 256-thread workgroup.  Each wave owns
-// 8 gates; each lane one column.  Digits of the lincomb'd mask coefficients
-// are staged in LDS per chunk of 32 coefficients; KSK rows are read once per
-// tile, coalesced (64 consecutive u64 per wave).
+// Tile: 32 gates x 64 output columns x one slice of the kN input coefficients
+// per 256-thread workgroup (split-K: the slices' partial sums are exact mod
+// 2^64, so they are combined with 64-bit atomic adds into a zeroed output).
+// Each wave owns 8 gates; each lane one output column.  Digits of the
+// lincomb'd mask coefficients are staged in LDS per chunk of 32 coefficients;
+// KSK rows are read once per tile, coalesced (64 consecutive u64 per wave).
 constexpr int KS_BT = 32, KS_CT = 64, KS_CH = 32;
 
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
 k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
-                    const uint64_t* __restrict__ ksk, int n, int big, uint64_t* __restrict__ out, int out_stride) {
+                    const uint64_t* __restrict__ ksk, int n, int big, int chunks_per_split,
+                    unsigned long long* __restrict__ out, int out_stride) {
     __shared__ int8_t dig[KS_BT][KS_CH][KSL];
     __shared__ DevGate sg[KS_BT];
     const int tid = threadIdx.x;
     const int col = blockIdx.y * KS_CT + (tid & 63);
     const int rg = tid >> 6;
     const int b0 = blockIdx.x * KS_BT;
+    const int c_begin = blockIdx.z * chunks_per_split * KS_CH;
+    const int c_end = min(big, c_begin + chunks_per_split * KS_CH);
     for (int e = tid; e < KS_BT; e += 256) {
         if (b0 + e < B) sg[e] = gates[b0 + e];
         else sg[e].n_in = 0, sg[e].offset = 0;
@@ -376,12 +343,12 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
     uint64_t acc[8];
 #pragma unroll
     for (int r = 0; r < 8; ++r) acc[r] = 0;
-    for (int i0 = 0; i0 < big; i0 += KS_CH) {
+    for (int i0 = c_begin; i0 < c_end; i0 += KS_CH) {
         __syncthreads();
         for (int e = tid; e < KS_BT * KS_CH; e += 256) {
             const int row = e / KS_CH, ii = e % KS_CH;
             uint64_t v = 0;
-            if (i0 + ii < big) {
+            if (i0 + ii < c_end) {
                 const DevGate& gg = sg[row];
                 for (int q = 0; q < gg.n_in; ++q)
                     v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i0 + ii];
@@ -393,7 +360,7 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
         }
         __syncthreads();
         if (col <= n) {
-            const int lim = big - i0 < KS_CH ? big - i0 : KS_CH;
+            const int lim = c_end - i0 < KS_CH ? c_end - i0 : KS_CH;
             for (int ii = 0; ii < lim; ++ii) {
 #pragma unroll
                 for (int j = 0; j < KSL; ++j) {
@@ -413,14 +380,15 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
             const int row = rg * 8 + r, b = b0 + row;
             if (b >= B) continue;
             uint64_t v = acc[r];
-            if (col == n) {
+            if (col == n && blockIdx.z == 0) {
                 const DevGate& gg = sg[row];
                 uint64_t body = (uint64_t)(int64_t)gg.offset << DELTA_LOG;
                 for (int q = 0; q < gg.n_in; ++q)
                     body += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + big];
                 v += body;
             }
-            out[(size_t)b * out_stride + col] = v;
+            if (gridDim.z == 1) out[(size_t)b * out_stride + col] = v;
+            else atomicAdd(&out[(size_t)b * out_stride + col], (unsigned long long)v);
         }
     }
 }
@@ -440,16 +408,37 @@ __global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, u
 // ================================================================== host side
 #define STREAM ((hipStream_t)stream_)
 
-template <int N, int K>
+template <int N, int K, int E>
 static void set_smem_attr() {
-    HIP_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate<N, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)br_smem_bytes<N, K>()));
-    HIP_CHECK(hipFuncSetAttribute((const void*)k_bsk_to_ntt<N, K>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)br_smem_bytes<N, K>()));
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate<N, K, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)br_smem_bytes<N, K, E>()));
+    HIP_CHECK(hipFuncSetAttribute((const void*)k_bsk_to_ntt<N, K, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)br_smem_bytes<N, K, E>()));
 }
 
 static bool supported(const Params& p) {
     return (p.N == 2048 && p.k == 1) || (p.N == 1024 && p.k == 2) || (p.N == 1024 && p.k == 1);
+}
+
+// run `body` with compile-time (N, K, E) matching the runtime parameters
+template <class F>
+static void dispatch(const Params& p, int E, F&& body) {
+    auto pick = [&](auto n, auto k, auto e) {
+        if (p.N == decltype(n)::value && p.k == decltype(k)::value && E == decltype(e)::value) {
+            body(n, k, e);
+            return true;
+        }
+        return false;
+    };
+    using I = std::integral_constant<int, 0>;
+    (void)sizeof(I);
+    if (pick(std::integral_constant<int, 2048>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 16>{})) return;
+    if (pick(std::integral_constant<int, 2048>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{})) return;
+    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 16>{})) return;
+    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 8>{})) return;
+    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 16>{})) return;
+    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{})) return;
+    throw Error(FR_ERR_INVALID, "device: no kernel variant for (N, k, E)");
 }
 
 Device::Device(const Params& p, int device) : p_(p), dev_(device) {
@@ -469,9 +458,9 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         HIP_CHECK(hipEventCreate(&ev));
         e = ev;
     }
-    if (p.N == 2048 && p.k == 1) set_smem_attr<2048, 1>();
-    if (p.N == 1024 && p.k == 2) set_smem_attr<1024, 2>();
-    if (p.N == 1024 && p.k == 1) set_smem_attr<1024, 1>();
+    if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
+    if (e_ != 8 && e_ != 16) throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS must be 8 or 16");
+    dispatch(p_, e_, [&](auto n, auto k, auto e) { set_smem_attr<decltype(n)::value, decltype(k)::value, decltype(e)::value>(); });
     // twiddles
     NttTables T(p.N);
     std::vector<uint64_t> tw(2 * (size_t)p.N);
@@ -504,7 +493,7 @@ std::string Device::info() const {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, dev_);
     std::ostringstream o;
-    o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount;
+    o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount << " E=" << e_;
     return o.str();
 }
 
@@ -580,34 +569,37 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
     HIP_CHECK(hipMalloc(&d_bsk_, 8 * bsk.size()));
     const uint64_t n_inv = gl_pow((uint64_t)p_.N, P - 2);
     const int blocks = p_.n * (p_.k + 1);
-    if (p_.N == 2048 && p_.k == 1)
-        k_bsk_to_ntt<2048, 1><<<blocks, 2 * 128, br_smem_bytes<2048, 1>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
-    else if (p_.N == 1024 && p_.k == 2)
-        k_bsk_to_ntt<1024, 2><<<blocks, 3 * 64, br_smem_bytes<1024, 2>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
-    else
-        k_bsk_to_ntt<1024, 1><<<blocks, 2 * 64, br_smem_bytes<1024, 1>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+    dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
+        constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
+        k_bsk_to_ntt<N, K, E><<<blocks, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+    });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(STREAM));
     HIP_CHECK(hipFree(coef));
 }
 
 void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
-    dim3 grid((unsigned)((n + KS_BT - 1) / KS_BT), (unsigned)((p_.n + 1 + KS_CT - 1) / KS_CT));
+    const int btiles = (int)((n + KS_BT - 1) / KS_BT);
+    const int ctiles = (p_.n + 1 + KS_CT - 1) / KS_CT;
+    const int chunks = (p_.big() + KS_CH - 1) / KS_CH;
+    // enough workgroups to fill 256 CUs several times over, in whole chunks
+    int splits = (2048 + btiles * ctiles - 1) / (btiles * ctiles);
+    splits = std::max(1, std::min(splits, chunks));
+    const int per = (chunks + splits - 1) / splits;
+    splits = (chunks + per - 1) / per;
+    if (splits > 1) HIP_CHECK(hipMemsetAsync(d_ks, 0, (size_t)8 * p_.ks_stride() * n, STREAM));
+    dim3 grid((unsigned)btiles, (unsigned)ctiles, (unsigned)splits);
     k_lincomb_keyswitch<3, 5><<<grid, 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_ksk_, p_.n,
-                                                         p_.big(), d_ks, p_.ks_stride());
+                                                         p_.big(), per, (unsigned long long*)d_ks, p_.ks_stride());
     HIP_CHECK(hipGetLastError());
 }
 
 void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
-    if (p_.N == 2048 && p_.k == 1)
-        k_blind_rotate<2048, 1><<<(unsigned)n, 256, br_smem_bytes<2048, 1>(), STREAM>>>(
+    dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
+        constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
+        k_blind_rotate<N, K, E><<<(unsigned)n, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(
             d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
-    else if (p_.N == 1024 && p_.k == 2)
-        k_blind_rotate<1024, 2><<<(unsigned)n, 192, br_smem_bytes<1024, 2>(), STREAM>>>(
-            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
-    else
-        k_blind_rotate<1024, 1><<<(unsigned)n, 128, br_smem_bytes<1024, 1>(), STREAM>>>(
-            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
+    });
     HIP_CHECK(hipGetLastError());
 }
 
@@ -707,14 +699,13 @@ void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, u
     HIP_CHECK(hipMemcpy(da, a, 8 * count * N, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(db, b, 8 * count * N, hipMemcpyHostToDevice));
     const uint64_t n_inv = gl_pow((uint64_t)N, P - 2);
-    if (N == 2048) {
-        size_t sm = 8 * (2 * (size_t)Geom<2048>::NP + 2 * 2048);
-        HIP_CHECK(hipFuncSetAttribute((const void*)k_ring_mul<2048>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-        k_ring_mul<2048><<<(unsigned)count, 256, sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
-    } else {
-        size_t sm = 8 * (2 * (size_t)Geom<1024>::NP + 2 * 1024);
-        k_ring_mul<1024><<<(unsigned)count, 128, sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
-    }
+    dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
+        constexpr int NN = decltype(n_)::value, E = decltype(e_c)::value;
+        (void)k_;
+        const size_t sm = 8 * (2 * (size_t)NttGeo<NN, E>::NP + (size_t)NN);
+        HIP_CHECK(hipFuncSetAttribute((const void*)k_ring_mul<NN, E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
+        k_ring_mul<NN, E><<<(unsigned)count, 2 * (NN / E), sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
+    });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(STREAM));
     HIP_CHECK(hipMemcpy(out, dout, 8 * count * N, hipMemcpyDeviceToHost));

@@ -25,7 +25,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libfheregex.so")
+LIB_PATH = os.environ.get("FHEREGEX_LIB") or os.path.join(HERE, "libfheregex.so")
 REPO = os.path.dirname(HERE)
 HEADER = os.path.join(REPO, "include", "fheregex.h")
 
