@@ -9,7 +9,9 @@ Ranks shard start offsets (weak scaling: 256 starts per GPU); for N > 1 the
 per-rank boolean results are all-gathered over RCCL and OR-reduced with one
 threshold bootstrap on rank 0 (inside the timed step).
 
-value = gate bootstraps executed by all ranks per second of wall time;
+value = gate bootstraps (blind rotations) executed by all ranks per second of
+wall time (multi-value bootstrapping lets one rotation serve several LUTs: the
+LUT-output rate is reported beside it, never as the value);
 ms_per_step = end-to-end match time.  roofline: blind-rotation kernel, HIP
 events on the library's stream over the timed region, algorithmic bytes per
 bootstrap n*(k+1)^2*l*N*8.  cpu_baseline: the CPU restatement
@@ -155,6 +157,7 @@ def main():
     barrier()
     t0 = time.perf_counter()
     pbs_local = 0
+    rot_local = 0
     br_ms = 0.0
     br_launches = 0
     br_gates = 0
@@ -165,6 +168,7 @@ def main():
     for i in range(args.steps):
         o, st, fp = step()
         pbs_local += st.pbs
+        rot_local += st.blind_rotations
         br_ms += st.br_kernel_ms
         br_launches += st.br_launches
         br_gates += st.br_gates
@@ -180,13 +184,15 @@ def main():
     ctx.set_profiling(False)
 
     if dist is not None:
-        tt = torch.tensor([elapsed, float(pbs_local + final_pbs_total)], dtype=torch.float64, device="cuda")
+        tt = torch.tensor([elapsed, float(pbs_local + final_pbs_total), float(rot_local + final_pbs_total)],
+                          dtype=torch.float64, device="cuda")
         mx = tt.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_pbs = float(mx[0]), float(tt[1])
+        elapsed, total_pbs, total_rot = float(mx[0]), float(tt[1]), float(tt[2])
     else:
         total_pbs = float(pbs_local + final_pbs_total)
+        total_rot = float(rot_local + final_pbs_total)
 
     result = None
     if rank == 0:
@@ -217,7 +223,7 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     line = {
         "metric": METRIC,
-        "value": total_pbs / elapsed,
+        "value": total_rot / elapsed,
         "unit": "gate-bootstraps/s",
         "n_gpus": world,
         "steps": args.steps,
@@ -232,7 +238,9 @@ def main():
                    "content_chars": L, "params": args.params, "lowering": args.lowering,
                    "parallelism": f"start-offset shards x{world}"},
         "match_ms": ms_per_step,
-        "pbs_per_match": total_pbs / args.steps,
+        "blind_rotations_per_match": total_rot / args.steps,
+        "lut_outputs_per_match": total_pbs / args.steps,
+        "lut_outputs_per_s": total_pbs / elapsed,
         "levels": levels,
         "host_ms_per_match": host_ms / args.steps,
         "result_decrypted": result,

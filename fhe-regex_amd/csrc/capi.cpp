@@ -1,6 +1,7 @@
 // extern "C" boundary (include/fheregex.h): context, keys, ciphertext handles,
 // eager gate ops (the smart_* replacements), the batched has_match engine.
 #include <chrono>
+#include <map>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -68,6 +69,7 @@ struct fr_ctx {
     std::vector<HandleRec> handles;
     std::vector<uint32_t> free_handles;
     int lowering = FR_LOWER_THRESHOLD;
+    bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
 
     Device& device() {
         if (!dev) throw Error(FR_ERR_NO_DEVICE, "host-only context: no HIP device");
@@ -101,6 +103,9 @@ struct fr_ctx {
 
 namespace fr {
 
+// LUTs whose multi-value factor w_f has sum(d^2) <= this share rotations
+constexpr int MV_MAX_NORM2 = 8;
+
 // ---------------------------------------------------------------- executor
 // Runs a PBS program whose negative sources refer to blocks of `inputs`
 // (input q = pos q: src = -(1 + q*4 + blk)).  Returns one slot per gate
@@ -127,8 +132,12 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
     for (size_t g = 0; g < gates.size(); ++g) slot[g] = dev.alloc_slot();
     std::vector<DevGate> batch;
     size_t maxw = 0;
+    uint64_t jobs = 0;
     for (int l = 1; l <= maxl; ++l) {
         batch.clear();
+        // input signature -> open job index (multi-value bootstrapping merges
+        // small-norm LUTs that read the same linear combination)
+        std::map<std::vector<int32_t>, size_t> open_job;
         for (int g : by_level[l]) {
             const PGate& G = gates[g];
             DevGate d;
@@ -158,15 +167,37 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
             }
             d.n_in = nin;
             d.offset = off;
-            std::memcpy(d.lut, G.lut, 16);
-            d.out_slot = slot[g];
+            const bool small = lut_w_norm2(G.lut) <= MV_MAX_NORM2;
+            if (small && ctx->multi_value) {
+                std::vector<int32_t> sig{nin, off};
+                for (int q = 0; q < nin; ++q) {
+                    sig.push_back(d.in_slot[q]);
+                    sig.push_back(d.in_w[q]);
+                }
+                auto it = open_job.find(sig);
+                if (it != open_job.end() && batch[it->second].n_out < MAX_OUT) {
+                    DevGate& J = batch[it->second];
+                    std::memcpy(J.lut[J.n_out], G.lut, 16);
+                    J.out_slot[J.n_out] = slot[g];
+                    J.n_out++;
+                    J.direct = 0;
+                    continue;
+                }
+                open_job[sig] = batch.size();
+            }
+            std::memcpy(d.lut[0], G.lut, 16);
+            d.n_out = 1;
+            d.direct = 1;
+            d.out_slot[0] = slot[g];
             batch.push_back(d);
         }
         maxw = std::max(maxw, batch.size());
+        jobs += batch.size();
         dev.run_level(batch.data(), batch.size());
     }
     if (st) {
         st->pbs += gates.size();
+        st->blind_rotations += jobs;
         st->levels += (uint64_t)maxl;
         st->max_level_width = std::max<uint64_t>(st->max_level_width, maxw);
     }
@@ -189,9 +220,9 @@ static fr_ct finish_output(fr_ctx* ctx, const Program& prog, std::vector<int>& s
         d.in_slot[0] = slots[prog.out_gate];
         d.in_w[0] = prog.out_w;
         d.offset = prog.out_const;
-        d.out_slot = ctx->device().alloc_slot();
+        d.out_slot[0] = ctx->device().alloc_slot();
         ctx->device().run_linear(d);
-        r.b[0].slot = d.out_slot;
+        r.b[0].slot = d.out_slot[0];
     }
     for (int s : slots)
         if (s >= 0) ctx->device().free_slot(s);
@@ -205,6 +236,7 @@ static fr_ct run_program(fr_ctx* ctx, const Program& prog, const std::vector<fr_
 }
 
 static int cblk(int pos, int blk) { return -(1 + pos * 4 + blk); }
+
 
 static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
                         fr_match_stats* st) {
@@ -233,6 +265,7 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
         st->cache_hits = rec.cache_hits;
         st->n_branches = rec.n_branches;
         st->pbs = local.pbs;
+        st->blind_rotations = local.blind_rotations;
         st->levels = local.levels;
         st->max_level_width = local.max_level_width;
         st->host_ms = t1 - t0;
@@ -337,6 +370,21 @@ int fr_set_lowering(fr_ctx* ctx, int32_t mode) {
     FR_TRY({
         NEED(ctx && (mode == FR_LOWER_FAITHFUL || mode == FR_LOWER_THRESHOLD));
         ctx->lowering = mode;
+    })
+}
+
+int fr_set_multi_value(fr_ctx* ctx, int32_t on) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->multi_value = on != 0;
+    })
+}
+
+int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, int32_t n_out, int32_t direct,
+                              uint64_t* out) {
+    FR_TRY({
+        NEED(ctx && in && luts && out);
+        ctx->device().blind_rotate_multi_host(in, luts, n_out, direct, out);
     })
 }
 
@@ -574,10 +622,10 @@ int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out) {
                 d.in_slot[0] = ha.b[0].slot;
                 d.in_w[0] = -1;
                 d.offset = 1;
-                d.out_slot = ctx->device().alloc_slot();
+                d.out_slot[0] = ctx->device().alloc_slot();
                 ctx->device().run_linear(d);
                 ctx->device().sync();
-                r.b[0].slot = d.out_slot;
+                r.b[0].slot = d.out_slot[0];
             }
             *out = ctx->new_handle(r);
         } else {  // general radix: block 0 through a LUT, blocks 1..3 copied
@@ -597,9 +645,9 @@ int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out) {
                 d.n_in = 1;
                 d.in_slot[0] = ha.b[blk].slot;
                 d.in_w[0] = 1;
-                d.out_slot = ctx->device().alloc_slot();
+                d.out_slot[0] = ctx->device().alloc_slot();
                 ctx->device().run_linear(d);
-                r.b[blk].slot = d.out_slot;
+                r.b[blk].slot = d.out_slot[0];
             }
             ctx->device().sync();
             *out = ctx->new_handle(r);
@@ -631,10 +679,10 @@ int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out) {
             d.n_in = 1;
             d.in_slot[0] = ctx->get(inputs[0]).b[0].slot;
             d.in_w[0] = 1;
-            d.out_slot = ctx->device().alloc_slot();
+            d.out_slot[0] = ctx->device().alloc_slot();
             ctx->device().run_linear(d);
             ctx->device().sync();
-            r.b[0].slot = d.out_slot;
+            r.b[0].slot = d.out_slot[0];
             *out = ctx->new_handle(r);
             return FR_OK;
         }
@@ -794,9 +842,11 @@ int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, 
             }
             d.n_in = nin;
             d.offset = off;
-            lut_eq(d.lut, 1);
+            lut_eq(d.lut[0], 1);
+            d.n_out = 1;
+            d.direct = 1;
             outs[i] = dev.alloc_slot();
-            d.out_slot = outs[i];
+            d.out_slot[0] = outs[i];
         }
         dev.bench_pbs(gates, iters, br_ms, total_ms);
         for (int s : outs) dev.free_slot(s);

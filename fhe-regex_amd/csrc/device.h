@@ -7,22 +7,30 @@
 
 namespace fr {
 
-// One programmable bootstrap as the device sees it:
-//   out_slot <- PBS_lut( offset*2^59 + sum_q w_q * arena[in_slot_q] )
+constexpr int MAX_OUT = 8;
+// One blind-rotation job as the device sees it:
+//   c = offset*2^59 + sum_q w_q * arena[in_slot_q];  KS; blind rotation of the
+//   test polynomial; out_slot[f] <- LUT_f(c) for f < n_out.
+// direct = 1: the test polynomial is LUT_0's own (one output).  direct = 0:
+// multi-value bootstrapping, test polynomial (Delta/2)*sum_j X^j and one
+// sparse small-integer product w_f per output (see k_blind_rotate).
 struct DevGate {
     int32_t n_in;
     int32_t offset;
     int32_t in_slot[15];
     int32_t in_w[15];
-    uint8_t lut[16];
-    int32_t out_slot;
-    int32_t _pad;
+    int32_t n_out;
+    int32_t direct;
+    int32_t out_slot[MAX_OUT];
+    uint8_t lut[MAX_OUT][16];
 };
-static_assert(sizeof(DevGate) == 136 + 16, "DevGate layout");
+static_assert(sizeof(DevGate) == 296, "DevGate layout");
+// sum of squared w_f coefficients of a LUT (noise growth of its factored output)
+int lut_w_norm2(const uint8_t* lut);
 
 struct DeviceTimers {
     double br_ms = 0, ks_ms = 0;
-    uint64_t br_launches = 0, br_gates = 0;
+    uint64_t br_launches = 0, br_gates = 0, lut_outputs = 0;
 };
 
 class Device {
@@ -58,6 +66,8 @@ class Device {
     // single-stage entry points for parity tests
     void keyswitch_host(const uint64_t* in, size_t count, uint64_t* out);
     void blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_t count, uint64_t* out);
+    // one job with n_out LUTs on one keyswitched input (multi-value or direct)
+    void blind_rotate_multi_host(const uint64_t* ks_in, const uint8_t* luts, int n_out, int direct, uint64_t* out);
     void ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out);
     // repeated full-PBS batches on resident inputs (bench / roofline)
     void bench_pbs(const std::vector<DevGate>& gates, int iters, double* br_ms, double* total_ms);

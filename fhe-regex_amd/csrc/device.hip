@@ -139,7 +139,7 @@ __device__ __forceinline__ void inverse_ntt(uint64_t (&x)[E], uint64_t* row, con
 // ------------------------------------------------------------ blind rotation
 template <int N, int K, int E>
 constexpr size_t br_smem_bytes() {
-    return sizeof(uint64_t) * ((size_t)(K + 1) * NttGeo<N, E>::NP + (size_t)N) + 16 + 2 * 1024;
+    return sizeof(uint64_t) * ((size_t)(K + 1) * NttGeo<N, E>::NP + (size_t)N) + 16 * MAX_OUT + 2 * 1024;
 }
 template <int N, int K, int E>
 constexpr int br_threads() {
@@ -169,16 +169,18 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
     uint64_t* xbuf = smem;                   // (K+1) rows of NP
     uint64_t* zt = xbuf + (K + 1) * G::NP;   // N
-    uint8_t* lut = (uint8_t*)(zt + N);       // 16
-    uint16_t* abar = (uint16_t*)(lut + 16);  // n (<= 1024)
+    uint8_t* lut = (uint8_t*)(zt + N);                // 16 * n_out
+    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024)
 
     const int tid = threadIdx.x;
     const int P = tid / G::T, tl = tid % G::T;
     const int g = blockIdx.x;
     const uint64_t* in = ks + (size_t)g * ks_stride;
 
+    const int n_out = gates[g].n_out;
+    const bool direct = gates[g].direct != 0;
     for (int i = tid; i < N; i += NT) zt[i] = tw[i];
-    if (tid < 16) lut[tid] = gates[g].lut[tid];
+    for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
     const uint32_t bbar = mod_switch(in[n], G::LOG + 1);
     __syncthreads();
@@ -194,7 +196,8 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                 const int s = (G::template idx<0>(tl, m) + (int)bbar) & (2 * N - 1);
                 const int sp = s < N ? s : s - N;
                 const int mm = (sp + half) / box;
-                const uint64_t v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
+                uint64_t v = DELTA_P / 2;  // multi-value test polynomial (Delta/2) * u
+                if (direct) v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
                 acc[m] = s < N ? v : gl_neg(v);
             }
         }
@@ -243,16 +246,66 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     }
 
     // sample extract (coefficient 0) under the flattened key, then Z_p -> 2^64
-    uint64_t* out = arena + (size_t)gates[g].out_slot * slot_stride;
+    if (direct) {
+        uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const int j = G::template idx<0>(tl, m);
-        if (P < K) {
-            const int t = j == 0 ? 0 : N - j;
-            const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
-            out[P * N + t] = zp_to_torus(v);
-        } else if (j == 0) {
-            out[K * N] = zp_to_torus(acc[m]);
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            if (P < K) {
+                const int t = j == 0 ? 0 : N - j;
+                const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
+                out[P * N + t] = zp_to_torus(v);
+            } else if (j == 0) {
+                out[K * N] = zp_to_torus(acc[m]);
+            }
+        }
+        return;
+    }
+    // multi-value: acc_f = w_f * acc with w_f = sum_t d_t X^{pos_t} (small d_t)
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = acc[m];
+    __syncthreads();
+    constexpr int box = N / 16, half = box / 2;
+    for (int f = 0; f < n_out; ++f) {
+        const uint8_t* lf = lut + 16 * f;
+        uint64_t* out = arena + (size_t)gates[g].out_slot[f] * slot_stride;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            if (P == K && j != 0) continue;
+            // positive / negative parts of sum_t d_t * (X^pos_t A)[j], limb-split (< 2^42 each)
+            uint64_t pl = 0, ph = 0, nl = 0, nh = 0;
+            for (int tt = 1; tt <= 16; ++tt) {
+                int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+                if (d == 0) continue;  // uniform across the workgroup
+                const int pos = tt < 16 ? tt * box - half : N - half;
+                int src = j - pos;
+                if (src < 0) {
+                    src += N;
+                    d = -d;
+                }
+                const uint64_t v = row[G::pad(src)];
+                const uint64_t ad = (uint64_t)(d < 0 ? -d : d);
+                const uint64_t lo = (v & 0xFFFFFFFFULL) * ad, hi = (v >> 32) * ad;
+                if (d > 0) { pl += lo; ph += hi; } else { nl += lo; nh += hi; }
+            }
+            // value = (ph - nh) * 2^32 + (pl - nl)  (mod P)
+            const int64_t A = (int64_t)(pl - nl), Bv = (int64_t)(ph - nh);
+            const int64_t B1 = Bv >> 32;
+            const uint64_t B0 = (uint64_t)Bv & 0xFFFFFFFFULL;
+            const int64_t Cv = A + B1 * (int64_t)4294967296LL - B1;  // + B1 * (2^32 - 1)
+            const uint64_t u = B0 << 32;
+            uint64_t r = u + (uint64_t)Cv;
+            if (Cv >= 0 && r < u) r += EPS;
+            if (Cv < 0 && u < (uint64_t)(-Cv)) r -= EPS;
+            r = gd::canon(r);
+            if (P < K) {
+                const int t = j == 0 ? 0 : N - j;
+                out[P * N + t] = zp_to_torus(j == 0 ? r : gl_neg(r));
+            } else {
+                out[K * N] = zp_to_torus(r);
+            }
         }
     }
 }
@@ -397,7 +450,7 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
 __global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, uint64_t* __restrict__ arena,
                                                 int slot_stride, int len) {
     const DevGate gg = *g;
-    uint64_t* out = arena + (size_t)gg.out_slot * slot_stride;
+    uint64_t* out = arena + (size_t)gg.out_slot[0] * slot_stride;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < len; t += gridDim.x * 256) {
         uint64_t v = (t == len - 1) ? ((uint64_t)(int64_t)gg.offset << DELTA_LOG) : 0;
         for (int q = 0; q < gg.n_in; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + t];
@@ -608,8 +661,10 @@ void Device::run_level(const DevGate* gates, size_t n) {
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
     for (size_t i = 0; i < n; ++i) {
         const DevGate& g = gates[i];
-        if (g.n_in < 0 || g.n_in > 15 || g.out_slot < 0 || (size_t)g.out_slot >= next_slot_)
+        if (g.n_in < 0 || g.n_in > 15 || g.n_out < 1 || g.n_out > MAX_OUT || (g.direct && g.n_out != 1))
             throw Error(FR_ERR_INVALID, "device gate: bad descriptor");
+        for (int f = 0; f < g.n_out; ++f)
+            if (g.out_slot[f] < 0 || (size_t)g.out_slot[f] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad output slot");
         for (int q = 0; q < g.n_in; ++q)
             if (g.in_slot[q] < 0 || (size_t)g.in_slot[q] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad input slot");
     }
@@ -624,6 +679,9 @@ void Device::run_level(const DevGate* gates, size_t n) {
     launch_br(d_gates_, d_ks_, n);
     if (profiling_) {
         HIP_CHECK(hipEventRecord((hipEvent_t)ev_[2], STREAM));
+        size_t outs = 0;
+        for (size_t i = 0; i < n; ++i) outs += gates[i].n_out;
+        timers_.lut_outputs += outs;
         HIP_CHECK(hipEventSynchronize((hipEvent_t)ev_[2]));
         float ks = 0, br = 0;
         HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
@@ -658,6 +716,9 @@ void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
         gates[i].n_in = 1;
         gates[i].in_slot[0] = slots[i];
         gates[i].in_w[0] = 1;
+        gates[i].n_out = 1;
+        gates[i].direct = 1;
+        gates[i].out_slot[0] = slots[i];
     }
     ensure_batch(count);
     HIP_CHECK(hipMemcpy(d_gates_, gates.data(), sizeof(DevGate) * count, hipMemcpyHostToDevice));
@@ -680,14 +741,46 @@ void Device::blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_
     for (size_t i = 0; i < count; ++i) {
         slots[i] = alloc_slot();
         std::memset(&gates[i], 0, sizeof(DevGate));
-        std::memcpy(gates[i].lut, luts + 16 * i, 16);
-        gates[i].out_slot = slots[i];
+        std::memcpy(gates[i].lut[0], luts + 16 * i, 16);
+        gates[i].n_out = 1;
+        gates[i].direct = 1;
+        gates[i].out_slot[0] = slots[i];
     }
     HIP_CHECK(hipMemcpy(d_gates_, gates.data(), sizeof(DevGate) * count, hipMemcpyHostToDevice));
     launch_br(d_gates_, d_ks_, count);
     HIP_CHECK(hipStreamSynchronize(STREAM));
     for (size_t i = 0; i < count; ++i) read_slot(slots[i], out + i * p_.lwe_len());
     for (int s : slots) free_slot(s);
+}
+
+void Device::blind_rotate_multi_host(const uint64_t* ks_in, const uint8_t* luts, int n_out, int direct,
+                                     uint64_t* out) {
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    if (n_out < 1 || n_out > MAX_OUT || (direct && n_out != 1)) throw Error(FR_ERR_INVALID, "bad n_out");
+    ensure_batch(1);
+    HIP_CHECK(hipMemcpy(d_ks_, ks_in, 8 * (size_t)(p_.n + 1), hipMemcpyHostToDevice));
+    DevGate g;
+    std::memset(&g, 0, sizeof g);
+    g.n_out = n_out;
+    g.direct = direct;
+    std::vector<int> slots(n_out);
+    for (int f = 0; f < n_out; ++f) {
+        slots[f] = alloc_slot();
+        g.out_slot[f] = slots[f];
+        std::memcpy(g.lut[f], luts + 16 * f, 16);
+    }
+    HIP_CHECK(hipMemcpy(d_gates_, &g, sizeof g, hipMemcpyHostToDevice));
+    launch_br(d_gates_, d_ks_, 1);
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    for (int f = 0; f < n_out; ++f) read_slot(slots[f], out + (size_t)f * p_.lwe_len());
+    for (int sl : slots) free_slot(sl);
+}
+
+int lut_w_norm2(const uint8_t* lut) {
+    int s = 0;
+    for (int m = 1; m < 16; ++m) s += ((int)lut[m] - lut[m - 1]) * ((int)lut[m] - lut[m - 1]);
+    s += ((int)lut[0] + lut[15]) * ((int)lut[0] + lut[15]);
+    return s;
 }
 
 void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out) {

@@ -84,5 +84,60 @@ __device__ __forceinline__ void gs(uint64_t& u, uint64_t& v, uint64_t z) {
     v = mul(d, z);
 }
 
+
+// ---- variant 2: explicit 32-bit carry chains --------------------------------
+__device__ __forceinline__ void mulw2(uint64_t a, uint64_t b, uint64_t& hi, uint64_t& lo) {
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0, p01 = (uint64_t)a0 * b1, p10 = (uint64_t)a1 * b0, p11 = (uint64_t)a1 * b1;
+    unsigned c1, c2, c3, c4;
+    uint32_t m = __builtin_addc((uint32_t)(p00 >> 32), (uint32_t)p01, 0u, &c1);
+    m = __builtin_addc(m, (uint32_t)p10, 0u, &c2);
+    uint32_t h0 = __builtin_addc((uint32_t)p11, (uint32_t)(p01 >> 32), c1, &c3);
+    h0 = __builtin_addc(h0, (uint32_t)(p10 >> 32), c2, &c4);
+    const uint32_t h1 = (uint32_t)(p11 >> 32) + c3 + c4;
+    lo = ((uint64_t)m << 32) | (uint32_t)p00;
+    hi = ((uint64_t)h1 << 32) | h0;
+}
+// hi*2^64 + lo = lo + hl*2^32 - (hh + hl)  (mod P); one net +-(2^32-1) fix-up
+__device__ __forceinline__ uint64_t red2(uint64_t hi, uint64_t lo) {
+    const uint32_t l0 = (uint32_t)lo, l1 = (uint32_t)(lo >> 32), hl = (uint32_t)hi, hh = (uint32_t)(hi >> 32);
+    unsigned c1, cs, b1, b2;
+    const uint32_t u1 = __builtin_addc(l1, hl, 0u, &c1);  // u = lo + hl*2^32 (carry c1 = 2^64)
+    const uint32_t s0 = __builtin_addc(hh, hl, 0u, &cs);  // S = hh + hl (33 bits)
+    const uint32_t r0 = __builtin_subc(l0, s0, 0u, &b1);
+    const uint32_t r1 = __builtin_subc(u1, cs, b1, &b2);  // r = u - S (borrow b2 = -2^64)
+    const uint64_t r = ((uint64_t)r1 << 32) | r0;
+    const uint64_t d = (c1 & ~b2) ? EPS : ((b2 & ~c1) ? (0ULL - EPS) : 0ULL);
+    return r + d;
+}
+__device__ __forceinline__ uint64_t mul2(uint64_t a, uint64_t b) {
+    uint64_t hi, lo;
+    mulw2(a, b, hi, lo);
+    return red2(hi, lo);
+}
+// x + t, t canonical: single wrap corrected by + (2^32-1)
+__device__ __forceinline__ uint64_t add_c2(uint64_t x, uint64_t t) {
+    unsigned c0, c;
+    const uint32_t s0 = __builtin_addc((uint32_t)x, (uint32_t)t, 0u, &c0);
+    const uint32_t s1 = __builtin_addc((uint32_t)(x >> 32), (uint32_t)(t >> 32), c0, &c);
+    return (((uint64_t)s1 << 32) | s0) + (c ? EPS : 0ULL);
+}
+__device__ __forceinline__ uint64_t sub_c2(uint64_t x, uint64_t t) {
+    unsigned b0, b;
+    const uint32_t d0 = __builtin_subc((uint32_t)x, (uint32_t)t, 0u, &b0);
+    const uint32_t d1 = __builtin_subc((uint32_t)(x >> 32), (uint32_t)(t >> 32), b0, &b);
+    return (((uint64_t)d1 << 32) | d0) - (b ? EPS : 0ULL);
+}
+__device__ __forceinline__ void ct2(uint64_t& x, uint64_t& y, uint64_t z) {
+    const uint64_t t = canon(mul2(z, y));
+    y = sub_c2(x, t);
+    x = add_c2(x, t);
+}
+__device__ __forceinline__ void gs2(uint64_t& u, uint64_t& v, uint64_t z) {
+    const uint64_t d = sub_g(v, u);
+    u = add_g(u, v);
+    v = mul2(d, z);
+}
+
 }  // namespace gd
 }  // namespace fr

@@ -61,7 +61,7 @@ class Params(C.Structure):
 
 class MatchStats(C.Structure):
     _fields_ = [("ct_ops", C.c_uint64), ("cache_hits", C.c_uint64), ("n_branches", C.c_uint64),
-                ("pbs", C.c_uint64), ("levels", C.c_uint64), ("max_level_width", C.c_uint64),
+                ("pbs", C.c_uint64), ("blind_rotations", C.c_uint64), ("levels", C.c_uint64), ("max_level_width", C.c_uint64),
                 ("host_ms", C.c_double), ("device_ms", C.c_double), ("br_kernel_ms", C.c_double),
                 ("ks_kernel_ms", C.c_double), ("br_launches", C.c_uint64), ("br_gates", C.c_uint64)]
 
@@ -120,6 +120,8 @@ _SIGS = {
                                  C.POINTER(PlainResult)]),
     "fr_set_lowering": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_set_profiling": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_set_multi_value": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_dev_blind_rotate_multi": (C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_uint8), C.c_int32, C.c_int32, u64p]),
     "fr_dev_keyswitch": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p]),
     "fr_dev_blind_rotate": (C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_uint8), C.c_size_t, u64p]),
     "fr_dev_ring_mul": (C.c_int, [C.c_void_p, u64p, u64p, C.c_size_t, u64p]),
@@ -234,6 +236,9 @@ class Context:
     def set_lowering(self, mode: int):
         _check(lib().fr_set_lowering(self.h, mode))
 
+    def set_multi_value(self, on: bool):
+        _check(lib().fr_set_multi_value(self.h, int(on)))
+
     def set_profiling(self, on: bool):
         _check(lib().fr_set_profiling(self.h, int(on)))
 
@@ -343,6 +348,14 @@ class Context:
         l = np.ascontiguousarray(np.asarray(luts, dtype=np.uint8).reshape(a.shape[0], 16))
         out = np.zeros((a.shape[0], self.lwe_len), dtype=np.uint64)
         _check(lib().fr_dev_blind_rotate(self.h, _p(a), l.ctypes.data_as(C.POINTER(C.c_uint8)), a.shape[0], _p(out)))
+        return out
+
+    def dev_blind_rotate_multi(self, ks: np.ndarray, luts, direct: bool = False) -> np.ndarray:
+        a = np.ascontiguousarray(ks.reshape(self.params.n + 1), dtype=np.uint64)
+        l = np.ascontiguousarray(np.asarray(luts, dtype=np.uint8).reshape(-1, 16))
+        out = np.zeros((l.shape[0], self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_dev_blind_rotate_multi(self.h, _p(a), l.ctypes.data_as(C.POINTER(C.c_uint8)), l.shape[0],
+                                               int(direct), _p(out)))
         return out
 
     def dev_ring_mul(self, a: np.ndarray, b: np.ndarray) -> np.ndarray:

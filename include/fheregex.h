@@ -77,7 +77,8 @@ typedef struct {
     uint64_t ct_ops;        /* reference Execution::ct_operations_count (execution.rs:56-58) */
     uint64_t cache_hits;    /* reference Execution::cache_hits (execution.rs:60-62) */
     uint64_t n_branches;    /* variants enumerated by build_branches (engine.rs:15-18) */
-    uint64_t pbs;           /* gate bootstraps actually executed */
+    uint64_t pbs;           /* LUT evaluations (gate outputs) executed */
+    uint64_t blind_rotations; /* blind rotations (several LUTs may share one: multi-value bootstrapping) */
     uint64_t levels;        /* dependent PBS levels (launch batches) */
     uint64_t max_level_width;
     double host_ms;         /* parse + enumerate + record + lower */
@@ -178,6 +179,9 @@ int fr_plain_match(const char* content, size_t len, const char* pattern, size_t 
 /* lowering modes for fr_plain_match / fr_set_lowering */
 enum { FR_LOWER_FAITHFUL = 0, FR_LOWER_THRESHOLD = 1 };
 int fr_set_lowering(fr_ctx* ctx, int32_t mode);
+/* Multi-value bootstrapping: gates of one level that read the same linear
+ * combination share one blind rotation (default on). */
+int fr_set_multi_value(fr_ctx* ctx, int32_t on);
 /* Device profiling with HIP events around every launch (adds a sync per level). */
 int fr_set_profiling(fr_ctx* ctx, int32_t on);
 
@@ -186,6 +190,10 @@ int fr_set_profiling(fr_ctx* ctx, int32_t on);
 int fr_dev_keyswitch(fr_ctx* ctx, const uint64_t* in, size_t count, uint64_t* out);
 /* in: count*(n+1) keyswitched LWEs, luts: count*16 -> out: count*(kN+1) */
 int fr_dev_blind_rotate(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, size_t count, uint64_t* out);
+/* one blind rotation with n_out LUTs (direct: n_out == 1, LUT polynomial
+ * rotated itself; else multi-value) -> out: n_out*(kN+1) */
+int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, int32_t n_out, int32_t direct,
+                              uint64_t* out);
 /* negacyclic product in Z_p[X]/(X^N+1) through the device NTT: count pairs */
 int fr_dev_ring_mul(fr_ctx* ctx, const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out);
 /* Full timed PBS batch for roofline measurement: count gates of the given

@@ -27,7 +27,18 @@ class Params(C.Structure):
 
 class Gate(C.Structure):
     _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("in_idx", C.c_int32 * 16),
-                ("in_w", C.c_int32 * 16), ("lut", C.c_uint8 * 16)]
+                ("in_w", C.c_int32 * 16), ("n_out", C.c_int32), ("direct", C.c_int32),
+                ("lut", (C.c_uint8 * 16) * 8)]
+
+
+def lut_terms(N: int, lut) -> list:
+    """w_f of the multi-value factorization: [(position, coefficient)]."""
+    box, half = N // 16, N // 32
+    t = [(m * box - half, int(lut[m]) - int(lut[m - 1])) for m in range(1, 16) if lut[m] != lut[m - 1]]
+    dd = -(int(lut[0]) + int(lut[15]))
+    if dd:
+        t.append((N - half, dd))
+    return t
 
 
 def build():
@@ -70,8 +81,11 @@ def lib():
         L.or_bsk_prepare.argtypes = [C.POINTER(Params), u64p]
         L.or_bsk_free.argtypes = [C.c_void_p]
         L.or_blind_rotate.argtypes = [C.c_void_p, u64p, C.POINTER(C.c_uint8), u64p]
+        L.or_blind_rotate_multi.argtypes = [C.c_void_p, u64p, C.POINTER(C.c_uint8), C.c_int, C.c_int, u64p]
+        L.or_lut_terms.restype = C.c_int
+        L.or_lut_terms.argtypes = [C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.or_lincomb.argtypes = [C.c_int, C.POINTER(Gate), u64p, u64p]
-        L.or_gates.argtypes = [C.c_void_p, u64p, C.POINTER(Gate), C.c_size_t, u64p, u64p]
+        L.or_gates.argtypes = [C.c_void_p, u64p, C.POINTER(Gate), C.c_size_t, u64p, C.POINTER(C.c_int32), u64p]
         L.or_num_threads.restype = C.c_int
         L.or_set_threads.argtypes = [C.c_int]
         _lib = L
@@ -194,21 +208,42 @@ class Oracle:
         lib().or_blind_rotate(self._pk, ptr(a), l, ptr(out))
         return out
 
+    def blind_rotate_multi(self, ks_lwe: np.ndarray, luts, direct: bool = False) -> np.ndarray:
+        luts = [list(l) for l in luts]
+        assert 1 <= len(luts) <= 8 and (not direct or len(luts) == 1)
+        flat = (C.c_uint8 * (16 * len(luts)))(*[v for l in luts for v in l])
+        out = np.zeros((len(luts), self.big + 1), dtype=np.uint64)
+        a = np.ascontiguousarray(ks_lwe, dtype=np.uint64)
+        lib().or_blind_rotate_multi(self._pk, ptr(a), flat, len(luts), int(direct), ptr(out))
+        return out
+
     def gates(self, gates, slots: np.ndarray) -> np.ndarray:
-        """gates: list of (inputs [(slot, weight)], offset, lut[16])."""
+        """gates: list of (inputs [(slot, weight)], offset, luts, direct) jobs; a
+        bare 16-entry lut means one direct output.  Returns all outputs, job-major."""
         arr = (Gate * len(gates))()
-        for q, (ins, off, lut) in enumerate(gates):
+        first = (C.c_int32 * len(gates))()
+        total = 0
+        for q, job in enumerate(gates):
+            ins, off, luts = job[0], job[1], job[2]
+            direct = job[3] if len(job) > 3 else None
+            if len(luts) == 16 and not isinstance(luts[0], (list, tuple)):
+                luts, direct = [luts], True if direct is None else direct
             g = arr[q]
             g.n_in = len(ins)
             g.offset = off
             for t, (i, w) in enumerate(ins):
                 g.in_idx[t] = i
                 g.in_w[t] = w
-            for t in range(16):
-                g.lut[t] = lut[t]
+            g.n_out = len(luts)
+            g.direct = int(bool(direct))
+            for f, lut in enumerate(luts):
+                for t in range(16):
+                    g.lut[f][t] = lut[t]
+            first[q] = total
+            total += len(luts)
         s = np.ascontiguousarray(slots.reshape(-1, self.big + 1), dtype=np.uint64)
-        out = np.zeros((len(gates), self.big + 1), dtype=np.uint64)
-        lib().or_gates(self._pk, ptr(self.ksk), arr, len(gates), ptr(s), ptr(out))
+        out = np.zeros((total, self.big + 1), dtype=np.uint64)
+        lib().or_gates(self._pk, ptr(self.ksk), arr, len(gates), ptr(s), first, ptr(out))
         return out
 
 

@@ -385,18 +385,51 @@ static inline uint64_t rot_coef(const uint64_t* poly, int N, int j, int a) {
     return s < N ? poly[s] : (poly[s - N] ? GL_P - poly[s - N] : 0);
 }
 
-/* Blind rotation + sample extract + Z_p -> 2^64 conversion of one keyswitched LWE. */
-void or_blind_rotate(void* pk, const uint64_t* ks_lwe, const uint8_t lut[16], uint64_t* out) {
+/* Multi-value bootstrapping (Carpov, Izabachene, Mollimard, CT-RSA 2019):
+ * with u(X) = sum_j X^j, u*(1-X) = 2 in Z[X]/(X^N+1), so every LUT polynomial
+ * factors as V_f = (Delta/2) u * w_f where w_f is sparse with small integer
+ * coefficients: f(m)-f(m-1) at m*box - box/2 (m = 1..15) and -(f(0)+f(15)) at
+ * N - box/2.  One blind rotation of TV = (Delta_p/2) u then yields every LUT
+ * on the same input: acc_f = w_f * acc (noise grows by ||w_f||_2).
+ * "direct" jobs rotate V_f itself (one output, no w-step). */
+int or_lut_terms(int N, const uint8_t lut[16], int32_t* pos, int32_t* d) {
+    int box = N / 16, half = box / 2, n = 0;
+    for (int m = 1; m < 16; m++) {
+        int dd = (int)lut[m] - (int)lut[m - 1];
+        if (dd) { pos[n] = m * box - half; d[n] = dd; n++; }
+    }
+    int dd = -((int)lut[0] + (int)lut[15]);
+    if (dd) { pos[n] = N - half; d[n] = dd; n++; }
+    return n;
+}
+/* sum_t d_t * (X^pos_t * poly)[j]  mod p */
+static uint64_t apply_w(const uint64_t* poly, int N, int j, int nt, const int32_t* pos, const int32_t* d) {
+    __int128 s = 0;
+    for (int t = 0; t < nt; t++) {
+        int src = j - pos[t];
+        __int128 v;
+        if (src >= 0) v = (__int128)poly[src];
+        else v = -(__int128)poly[src + N];
+        s += v * d[t];
+    }
+    s %= (__int128)GL_P;
+    if (s < 0) s += GL_P;
+    return (uint64_t)s;
+}
+
+/* Blind rotation of one keyswitched LWE, then for each of n_out LUTs the
+ * w-step (unless direct), sample extract and Z_p -> 2^64 conversion. */
+void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts, int n_out, int direct, uint64_t* outs) {
     or_bsk* K = (or_bsk*)pk;
     const or_params* P = &K->P;
     int k = P->k, N = P->N, n = P->n, log2N2 = ilog2(2 * N);
-    size_t kp1 = (size_t)k + 1;
+    size_t kp1 = (size_t)k + 1, big = (size_t)k * N;
     uint64_t* acc = calloc(kp1 * N, 8);
-    uint64_t* rot = malloc(8 * N);
     uint64_t* D = malloc(8 * kp1 * N);
     uint64_t* res = malloc(8 * N);
     uint64_t* V = malloc(8 * N);
-    make_lut_poly(N, lut, V);
+    if (direct) make_lut_poly(N, luts, V);
+    else for (int j = 0; j < N; j++) V[j] = DELTA_P / 2;
     uint32_t b = mod_switch(ks_lwe[n], log2N2);
     /* acc = (0, X^{-b} V) */
     for (int j = 0; j < N; j++) acc[(size_t)k * N + j] = rot_coef(V, N, j, (2 * N - (int)b) % (2 * N));
@@ -420,26 +453,42 @@ void or_blind_rotate(void* pk, const uint64_t* ks_lwe, const uint8_t lut[16], ui
             for (int t = 0; t < N; t++) acc[c * N + t] = gl_add(acc[c * N + t], res[t]);
         }
     }
-    /* sample extract (coefficient 0) under the flattened key, then to 2^64 */
-    for (int j = 0; j < k; j++) {
-        const uint64_t* A = acc + (size_t)j * N;
-        for (int t = 0; t < N; t++) {
-            uint64_t v = t == 0 ? A[0] : (A[N - t] ? GL_P - A[N - t] : 0);
-            out[(size_t)j * N + t] = or_conv(v);
+    int32_t pos[17], d[17];
+    for (int f = 0; f < (direct ? 1 : n_out); f++) {
+        uint64_t* out = outs + (size_t)f * (big + 1);
+        int nt = direct ? 0 : or_lut_terms(N, luts + 16 * f, pos, d);
+        /* sample extract (coefficient 0) under the flattened key, then to 2^64 */
+        for (int j = 0; j < k; j++) {
+            const uint64_t* A = acc + (size_t)j * N;
+            for (int t = 0; t < N; t++) {
+                int src = t == 0 ? 0 : N - t;
+                uint64_t a = direct ? A[src] : apply_w(A, N, src, nt, pos, d);
+                uint64_t v = t == 0 ? a : (a ? GL_P - a : 0);
+                out[(size_t)j * N + t] = or_conv(v);
+            }
         }
+        const uint64_t* B = acc + (size_t)k * N;
+        out[big] = or_conv(direct ? B[0] : apply_w(B, N, 0, nt, pos, d));
     }
-    out[(size_t)k * N] = or_conv(acc[(size_t)k * N]);
-    free(acc); free(rot); free(D); free(res); free(V);
+    free(acc); free(D); free(res); free(V);
+}
+
+/* single LUT, rotating the LUT polynomial itself */
+void or_blind_rotate(void* pk, const uint64_t* ks_lwe, const uint8_t lut[16], uint64_t* out) {
+    or_blind_rotate_multi(pk, ks_lwe, lut, 1, 1, out);
 }
 
 /* ------------------------------------------------------------------ gates */
-/* A gate: c = offset*2^59 + sum_i w_i * in_i (mod 2^64), then PBS with lut. */
+/* A rotation job: c = offset*2^59 + sum_i w_i * in_i (mod 2^64), then one
+ * blind rotation and n_out LUT outputs (factored unless direct). */
 typedef struct {
     int32_t n_in;
     int32_t offset;
     int32_t in_idx[16];
     int32_t in_w[16];
-    uint8_t lut[16];
+    int32_t n_out;
+    int32_t direct;
+    uint8_t lut[8][16];
 } or_gate;
 
 void or_lincomb(int big, const or_gate* g, const uint64_t* slots, uint64_t* out) {
@@ -452,8 +501,10 @@ void or_lincomb(int big, const or_gate* g, const uint64_t* slots, uint64_t* out)
     }
 }
 
-/* Evaluate `count` independent gates over `slots` (LWE big, torus 2^64), OpenMP. */
-void or_gates(void* pk, const uint64_t* ksk, const or_gate* gates, size_t count, const uint64_t* slots, uint64_t* out) {
+/* Evaluate `count` independent jobs over `slots` (LWE big, torus 2^64), OpenMP.
+ * Outputs of job q start at out + out_first[q] * (kN+1). */
+void or_gates(void* pk, const uint64_t* ksk, const or_gate* gates, size_t count, const uint64_t* slots,
+              const int32_t* out_first, uint64_t* out) {
     or_bsk* K = (or_bsk*)pk;
     int big = K->P.k * K->P.N, n = K->P.n;
     #pragma omp parallel
@@ -464,7 +515,8 @@ void or_gates(void* pk, const uint64_t* ksk, const or_gate* gates, size_t count,
         for (long q = 0; q < (long)count; q++) {
             or_lincomb(big, &gates[q], slots, lc);
             or_keyswitch(&K->P, ksk, lc, 1, ks);
-            or_blind_rotate(pk, ks, gates[q].lut, out + (size_t)q * (big + 1));
+            or_blind_rotate_multi(pk, ks, &gates[q].lut[0][0], gates[q].n_out, gates[q].direct,
+                                  out + (size_t)out_first[q] * (big + 1));
         }
         free(lc); free(ks);
     }

@@ -71,6 +71,34 @@ def test_blind_rotate_bit_exact(gctx, oracle_k1):
         assert O.decode16(got[i])[0] == luts[i][[5, 12, 0][i]]
 
 
+def test_multi_value_blind_rotate_bit_exact(gctx, oracle_k1):
+    O = oracle_k1
+    ks = O.keyswitch(O.encrypt_blocks([6, 13], seed=55))
+    luts = [[int(v == 6) for v in range(16)], [int(v in (6, 13)) for v in range(16)], [int(v >= 9) for v in range(16)],
+            [int(v == 13) for v in range(16)], [int(v % 2 == 0) for v in range(16)]]
+    for i, m in enumerate([6, 13]):
+        got = gctx.dev_blind_rotate_multi(ks[i], luts)
+        exp = O.blind_rotate_multi(ks[i], luts)
+        assert (got == exp).all(), i
+        assert [int(O.decode16(o)[0]) for o in got] == [l[m] for l in luts]
+
+
+def test_executor_merges_same_input_gates(gctx):
+    rng = np.random.default_rng(12)
+    s = "".join(chr(c) for c in rng.integers(0x20, 0x7F, 40))
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=12))
+    out, st = gctx.has_match(hs, "/abc/")
+    assert st.blind_rotations < st.pbs  # lo-nibble tests for a, b, c share one rotation per char
+    assert gctx.decrypt_radix(gctx.download_radix(out)) == ro.has_match(s, "/abc/").result
+    gctx.set_multi_value(False)
+    try:
+        out2, st2 = gctx.has_match(hs, "/abc/")
+    finally:
+        gctx.set_multi_value(True)
+    assert st2.blind_rotations == st2.pbs == st.pbs
+    assert gctx.decrypt_radix(gctx.download_radix(out2)) == gctx.decrypt_radix(gctx.download_radix(out))
+
+
 def test_gate_program_bit_exact(gctx, oracle_k1):
     """Lincomb + KS + BR through fr_run_gates vs the oracle's gate evaluation."""
     O = oracle_k1

@@ -125,3 +125,31 @@ def test_oracle_pbs_lut(oracle_k1):
     assert [int(d) for d in dec] == [luts[i][msgs[i]] for i in range(4)]
     # trivial input: bootstrapping a trivial ciphertext yields a trivial (noiseless) one
     assert (out[3][:-1] == 0).all()
+
+
+def test_oracle_multi_value_bootstrap(oracle_k1):
+    """One rotation of (Delta/2)*u serves several LUTs (w_f factorization)."""
+    O = oracle_k1
+    ks = O.keyswitch(O.encrypt_blocks([7, 0], seed=41))
+    luts = [[int(v == 7) for v in range(16)], [int(v in (5, 7)) for v in range(16)], [int(v >= 3) for v in range(16)],
+            [int(v == 0) for v in range(16)]]
+    for i, m in enumerate([7, 0]):
+        outs = O.blind_rotate_multi(ks[i], luts)
+        assert [int(O.decode16(o)[0]) for o in outs] == [l[m] for l in luts]
+    # the factorization itself: (Delta/2) u * w_f == V_f in Z[X]/(X^N+1) (N small, exact)
+    N, box, half = 64, 4, 2
+    for lut in luts + [[(3 * v + 1) % 16 for v in range(16)]]:
+        V = [2 * (lut[(j + half) // box] if (j + half) // box < 16 else -lut[0]) for j in range(N)]
+        w = [0] * N
+        for pos, d in of.lut_terms(N, lut):
+            w[pos] += d
+        prod = [0] * N
+        for j in range(N):
+            for i, d in enumerate(w):
+                if d:
+                    k = i + j
+                    if k < N:
+                        prod[k] += d
+                    else:
+                        prod[k - N] -= d
+        assert prod == V
