@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
     ap.add_argument("--cpu-sample", type=int, default=32, help="gate bootstraps in the CPU baseline sample (0: skip)")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
+    ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -210,6 +211,14 @@ def main():
                   "pbs_per_s": 2 * args.saturate / (tot_sat / 1e3),
                   "br_pbs_per_s": 2 * args.saturate / (br_sat / 1e3)}
 
+    probe = None
+    if args.probe and rank == 0:
+        probe = {}
+        for cnt in [int(x) for x in args.probe.split(",")]:
+            hs = [handles[lo + (i % (win_hi - lo))] for i in range(cnt)]
+            br_p, tot_p = ctx.dev_bench_pbs(hs, 2)
+            probe[cnt] = {"br_ms": br_p / 2, "total_ms": tot_p / 2}
+
     if rank != 0:
         if dist is not None:
             dist.barrier()
@@ -259,6 +268,7 @@ def main():
             "br_gates_per_launch": br_gates / max(br_launches, 1),
         },
         "kernel_saturated": kernel,
+        "latency_probe": probe,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))

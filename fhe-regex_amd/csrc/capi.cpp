@@ -155,18 +155,26 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
                     const HandleRec& h = ctx->get(inputs[q]);
                     const Block& b = h.b[cb % 4];
                     if (b.slot < 0) {
-                        off += in.w * (int)b.triv;
+                        off += 2 * in.w * (int)b.triv;  // offsets are in units of Delta/2
                         continue;
                     }
                     s = b.slot;
                 }
-                if (nin >= 15) throw Error(FR_ERR_INVALID, "gate fan-in > 15");
+                if (nin >= 16) throw Error(FR_ERR_INVALID, "gate fan-in > 16");
                 d.in_slot[nin] = s;
                 d.in_w[nin] = in.w;
                 ++nin;
             }
             d.n_in = nin;
             d.offset = off;
+            if (G.kind == GATE_SIGN) {
+                d.n_out = 1;
+                d.direct = JOB_SIGN;
+                d.out_slot[0] = slot[g];
+                batch.push_back(d);
+                continue;
+            }
+            if (off & 1) throw Error(FR_ERR_INVALID, "LUT gate with a half-integral offset");
             const bool small = lut_w_norm2(G.lut) <= MV_MAX_NORM2;
             if (small && ctx->multi_value) {
                 std::vector<int32_t> sig{nin, off};
@@ -180,14 +188,14 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
                     std::memcpy(J.lut[J.n_out], G.lut, 16);
                     J.out_slot[J.n_out] = slot[g];
                     J.n_out++;
-                    J.direct = 0;
+                    J.direct = JOB_MULTI;
                     continue;
                 }
                 open_job[sig] = batch.size();
             }
             std::memcpy(d.lut[0], G.lut, 16);
             d.n_out = 1;
-            d.direct = 1;
+            d.direct = JOB_DIRECT;
             d.out_slot[0] = slot[g];
             batch.push_back(d);
         }
@@ -219,7 +227,7 @@ static fr_ct finish_output(fr_ctx* ctx, const Program& prog, std::vector<int>& s
         d.n_in = 1;
         d.in_slot[0] = slots[prog.out_gate];
         d.in_w[0] = prog.out_w;
-        d.offset = prog.out_const;
+        d.offset = 2 * prog.out_const;
         d.out_slot[0] = ctx->device().alloc_slot();
         ctx->device().run_linear(d);
         r.b[0].slot = d.out_slot[0];
@@ -621,7 +629,7 @@ int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out) {
                 d.n_in = 1;
                 d.in_slot[0] = ha.b[0].slot;
                 d.in_w[0] = -1;
-                d.offset = 1;
+                d.offset = 2;
                 d.out_slot[0] = ctx->device().alloc_slot();
                 ctx->device().run_linear(d);
                 ctx->device().sync();
@@ -686,7 +694,7 @@ int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out) {
             *out = ctx->new_handle(r);
             return FR_OK;
         }
-        // balanced tree of <= 15-input threshold ORs
+        // balanced tree of <= 16-input threshold ORs
         Program p;
         std::vector<int> cur;  // sources: negative = input q, else gate
         for (size_t q = 0; q < inputs.size(); ++q) cur.push_back(cblk((int)q, 0));
@@ -698,9 +706,10 @@ int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out) {
                 if (len == 1) {
                     next.push_back(cur[start]);
                 } else {
-                    PGate g;
+                    PGate g;  // OR of <= 16 booleans: sign of sum - 1/2
                     for (size_t t = 0; t < len; ++t) g.ins.push_back({cur[start + t], 1});
-                    lut_at_least(g.lut, 1);
+                    g.kind = GATE_SIGN;
+                    g.offset = -1;
                     p.gates.push_back(g);
                     next.push_back((int)p.gates.size() - 1);
                 }
@@ -730,8 +739,9 @@ int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n) {
         std::vector<PGate> pg(n);
         for (size_t j = 0; j < n; ++j) {
             const fr_gate& g = gates[j];
-            NEED(g.n_in >= 0 && g.n_in <= 15);
+            NEED(g.n_in >= 0 && g.n_in <= 16 && (g.kind == GATE_LUT || g.kind == GATE_SIGN));
             pg[j].offset = g.offset;
+            pg[j].kind = g.kind;
             std::memcpy(pg[j].lut, g.lut, 16);
             for (int q = 0; q < g.n_in; ++q) {
                 if (g.in[q] & 0x80000000u) {
@@ -841,10 +851,10 @@ int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, 
                 ++nin;
             }
             d.n_in = nin;
-            d.offset = off;
+            d.offset = 2 * off;
             lut_eq(d.lut[0], 1);
             d.n_out = 1;
-            d.direct = 1;
+            d.direct = JOB_DIRECT;
             outs[i] = dev.alloc_slot();
             d.out_slot[0] = outs[i];
         }

@@ -9,22 +9,25 @@ namespace fr {
 
 constexpr int MAX_OUT = 8;
 // One blind-rotation job as the device sees it:
-//   c = offset*2^59 + sum_q w_q * arena[in_slot_q];  KS; blind rotation of the
+//   c = offset*2^58 + sum_q w_q * arena[in_slot_q];  KS; blind rotation of the
 //   test polynomial; out_slot[f] <- LUT_f(c) for f < n_out.
 // direct = 1: the test polynomial is LUT_0's own (one output).  direct = 0:
 // multi-value bootstrapping, test polynomial (Delta/2)*sum_j X^j and one
 // sparse small-integer product w_f per output (see k_blind_rotate).
+// direct = 2: sign gate, test polynomial (Delta/2)*sum_j X^j, one output
+// [c > 0] obtained as +-Delta/2 + Delta/2.
+enum : int32_t { JOB_MULTI = 0, JOB_DIRECT = 1, JOB_SIGN = 2 };
 struct DevGate {
     int32_t n_in;
-    int32_t offset;
-    int32_t in_slot[15];
-    int32_t in_w[15];
+    int32_t offset;  // units of Delta/2 = 2^58
+    int32_t in_slot[16];
+    int32_t in_w[16];
     int32_t n_out;
     int32_t direct;
     int32_t out_slot[MAX_OUT];
     uint8_t lut[MAX_OUT][16];
 };
-static_assert(sizeof(DevGate) == 296, "DevGate layout");
+static_assert(sizeof(DevGate) == 304, "DevGate layout");
 // sum of squared w_f coefficients of a LUT (noise growth of its factored output)
 int lut_w_norm2(const uint8_t* lut);
 
@@ -56,7 +59,7 @@ class Device {
 
     // run one dependency level of gates (all independent), async on the stream
     void run_level(const DevGate* gates, size_t n);
-    // linear combination without bootstrap (NOT of a boolean): out = offset*2^59 + sum w*in
+    // linear combination without bootstrap (NOT of a boolean): out = offset*2^58 + sum w*in
     void run_linear(const DevGate& g);
     void sync();
 
@@ -82,7 +85,9 @@ class Device {
 
     Params p_;
     int dev_;
-    int e_ = 8;   // coefficients per lane in the NTT kernels (8 or 16)
+    int e_ = 8;        // coefficients per lane in the NTT kernels (4 or 8)
+    int e_small_ = 4;  // ... for launches of at most small_batch_ bootstraps
+    size_t small_batch_ = 256;
     void* stream_ = nullptr;  // hipStream_t
     uint64_t* d_ksk_ = nullptr;
     uint64_t* d_bsk_ = nullptr;  // NTT domain, scaled by 1/N

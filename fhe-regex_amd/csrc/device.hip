@@ -146,17 +146,18 @@ constexpr int br_threads() {
     return (K + 1) * (N / E);
 }
 
-// BSK slot layout for lane tl / register m of the last NTT phase: m*T + tl
+// BSK NTT-domain layout: natural (bit-reversed) slot order, the same for every
+// lane geometry E, so the lane count can be chosen per launch.
 template <int N, int E>
 __device__ __forceinline__ int bsk_pos(int tl, int m) {
-    return m * NttGeo<N, E>::T + tl;
+    return NttGeo<N, E>::template idx<NttGeo<N, E>::NPH - 1>(tl, m);
 }
 
 // minimum waves per SIMD: E=8 caps registers at 128 so two 512-thread
 // workgroups share a CU (measured +27% saturated throughput over 146 VGPRs)
 template <int E>
 constexpr int br_min_waves() {
-    return E == 8 ? 4 : 1;
+    return E == 8 ? 4 : E == 4 ? 4 : 1;
 }
 template <int N, int K, int E>
 __global__ void __launch_bounds__((K + 1) * (N / E), br_min_waves<E>())
@@ -178,7 +179,8 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     const uint64_t* in = ks + (size_t)g * ks_stride;
 
     const int n_out = gates[g].n_out;
-    const bool direct = gates[g].direct != 0;
+    const int kind = gates[g].direct;
+    const bool direct = kind == JOB_DIRECT;
     for (int i = tid; i < N; i += NT) zt[i] = tw[i];
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
@@ -246,8 +248,10 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     }
 
     // sample extract (coefficient 0) under the flattened key, then Z_p -> 2^64
-    if (direct) {
+    if (kind != JOB_MULTI) {
         uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
+        // sign gate: +-Delta/2 (+ Delta/2) -> {0, Delta}
+        const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int j = G::template idx<0>(tl, m);
@@ -256,7 +260,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                 const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
                 out[P * N + t] = zp_to_torus(v);
             } else if (j == 0) {
-                out[K * N] = zp_to_torus(acc[m]);
+                out[K * N] = zp_to_torus(acc[m]) + post;
             }
         }
         return;
@@ -435,7 +439,7 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
             uint64_t v = acc[r];
             if (col == n && blockIdx.z == 0) {
                 const DevGate& gg = sg[row];
-                uint64_t body = (uint64_t)(int64_t)gg.offset << DELTA_LOG;
+                uint64_t body = (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1);
                 for (int q = 0; q < gg.n_in; ++q)
                     body += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + big];
                 v += body;
@@ -452,7 +456,7 @@ __global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, u
     const DevGate gg = *g;
     uint64_t* out = arena + (size_t)gg.out_slot[0] * slot_stride;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < len; t += gridDim.x * 256) {
-        uint64_t v = (t == len - 1) ? ((uint64_t)(int64_t)gg.offset << DELTA_LOG) : 0;
+        uint64_t v = (t == len - 1) ? ((uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1)) : 0;
         for (int q = 0; q < gg.n_in; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + t];
         out[t] = v;
     }
@@ -483,14 +487,15 @@ static void dispatch(const Params& p, int E, F&& body) {
         }
         return false;
     };
-    using I = std::integral_constant<int, 0>;
-    (void)sizeof(I);
-    if (pick(std::integral_constant<int, 2048>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 16>{})) return;
-    if (pick(std::integral_constant<int, 2048>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{})) return;
-    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 16>{})) return;
-    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 2>{}, std::integral_constant<int, 8>{})) return;
-    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 16>{})) return;
-    if (pick(std::integral_constant<int, 1024>{}, std::integral_constant<int, 1>{}, std::integral_constant<int, 8>{})) return;
+    using I2048 = std::integral_constant<int, 2048>;
+    using I1024 = std::integral_constant<int, 1024>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    using E4 = std::integral_constant<int, 4>;
+    using E8 = std::integral_constant<int, 8>;
+    if (pick(I2048{}, I1{}, E8{}) || pick(I2048{}, I1{}, E4{})) return;
+    if (pick(I1024{}, I2{}, E8{}) || pick(I1024{}, I2{}, E4{})) return;
+    if (pick(I1024{}, I1{}, E8{}) || pick(I1024{}, I1{}, E4{})) return;
     throw Error(FR_ERR_INVALID, "device: no kernel variant for (N, k, E)");
 }
 
@@ -512,8 +517,12 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         e = ev;
     }
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
-    if (e_ != 8 && e_ != 16) throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS must be 8 or 16");
-    dispatch(p_, e_, [&](auto n, auto k, auto e) { set_smem_attr<decltype(n)::value, decltype(k)::value, decltype(e)::value>(); });
+    if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
+    if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
+    if ((e_ != 8 && e_ != 4) || (e_small_ != 8 && e_small_ != 4))
+        throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 4 or 8");
+    for (int e : {4, 8})
+        dispatch(p_, e, [&](auto n, auto k, auto ec) { set_smem_attr<decltype(n)::value, decltype(k)::value, decltype(ec)::value>(); });
     // twiddles
     NttTables T(p.N);
     std::vector<uint64_t> tw(2 * (size_t)p.N);
@@ -648,7 +657,9 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
 }
 
 void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
-    dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
+    // small levels (at most one bootstrap per CU): more lanes per bootstrap for latency
+    const int E = n <= small_batch_ ? e_small_ : e_;
+    dispatch(p_, E, [&](auto n_, auto k_, auto e_c) {
         constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
         k_blind_rotate<N, K, E><<<(unsigned)n, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(
             d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
@@ -661,7 +672,8 @@ void Device::run_level(const DevGate* gates, size_t n) {
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
     for (size_t i = 0; i < n; ++i) {
         const DevGate& g = gates[i];
-        if (g.n_in < 0 || g.n_in > 15 || g.n_out < 1 || g.n_out > MAX_OUT || (g.direct && g.n_out != 1))
+        if (g.n_in < 0 || g.n_in > 16 || g.n_out < 1 || g.n_out > MAX_OUT || g.direct < 0 || g.direct > 2 ||
+            (g.direct && g.n_out != 1))
             throw Error(FR_ERR_INVALID, "device gate: bad descriptor");
         for (int f = 0; f < g.n_out; ++f)
             if (g.out_slot[f] < 0 || (size_t)g.out_slot[f] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad output slot");
@@ -717,7 +729,7 @@ void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
         gates[i].in_slot[0] = slots[i];
         gates[i].in_w[0] = 1;
         gates[i].n_out = 1;
-        gates[i].direct = 1;
+        gates[i].direct = JOB_DIRECT;
         gates[i].out_slot[0] = slots[i];
     }
     ensure_batch(count);
@@ -743,7 +755,7 @@ void Device::blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_
         std::memset(&gates[i], 0, sizeof(DevGate));
         std::memcpy(gates[i].lut[0], luts + 16 * i, 16);
         gates[i].n_out = 1;
-        gates[i].direct = 1;
+        gates[i].direct = JOB_DIRECT;
         gates[i].out_slot[0] = slots[i];
     }
     HIP_CHECK(hipMemcpy(d_gates_, gates.data(), sizeof(DevGate) * count, hipMemcpyHostToDevice));
@@ -756,7 +768,8 @@ void Device::blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_
 void Device::blind_rotate_multi_host(const uint64_t* ks_in, const uint8_t* luts, int n_out, int direct,
                                      uint64_t* out) {
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
-    if (n_out < 1 || n_out > MAX_OUT || (direct && n_out != 1)) throw Error(FR_ERR_INVALID, "bad n_out");
+    if (n_out < 1 || n_out > MAX_OUT || direct < 0 || direct > 2 || (direct && n_out != 1))
+        throw Error(FR_ERR_INVALID, "bad n_out");
     ensure_batch(1);
     HIP_CHECK(hipMemcpy(d_ks_, ks_in, 8 * (size_t)(p_.n + 1), hipMemcpyHostToDevice));
     DevGate g;

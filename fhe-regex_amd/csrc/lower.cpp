@@ -76,7 +76,7 @@ struct Lowerer {
         PGate g;
         g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
         std::memcpy(g.lut, lut, 16);
-        std::vector<int64_t> key{6, pos, half};
+        std::vector<int64_t> key{6, pos, half};  // (offset 0, LUT kind)
         for (int v = 0; v < 16; ++v) key.push_back(lut[v]);
         return add_gate(key, g);
     }
@@ -180,10 +180,12 @@ struct Lowerer {
         if (b.k == Form::AND || b.k == Form::LIT) return b;
         return a;
     }
-    // AND / OR of literals as one threshold gate (m <= MAX_FANIN)
+    // AND / OR of m <= 16 literals as one SIGN gate:
+    //   AND: s = sum - m + 1/2 > 0 ;  OR: s = sum - 1/2 > 0   (s in (-16, 16))
     int threshold_gate(bool is_and, std::vector<Lit> lits) {
         std::sort(lits.begin(), lits.end());
         PGate g;
+        g.kind = GATE_SIGN;
         int negs = 0;
         std::vector<int64_t> key{2, is_and ? 1 : 0};
         for (auto& l : lits) {
@@ -191,8 +193,8 @@ struct Lowerer {
             negs += l.neg;
             key.push_back(l.gate * 2 + l.neg);
         }
-        g.offset = negs;
-        lut_at_least(g.lut, is_and ? (int)lits.size() : 1);
+        const int m = (int)lits.size();
+        g.offset = 2 * negs + (is_and ? 1 - 2 * m : -1);
         return add_gate(key, g);
     }
     Lit materialize(const Form& f0) {
@@ -375,7 +377,7 @@ struct Lowerer {
                             offset += l.neg;
                         }
                     }
-                    g.offset = offset;
+                    g.offset = 2 * offset;
                     if (is_and) lut_eq(g.lut, 2);
                     else lut_at_least(g.lut, 1);
                     f = lit_form(Lit{add_gate(key, g), false});
@@ -457,7 +459,7 @@ int eval_program(const Program& prog, const uint8_t* content, size_t L) {
     std::vector<int> val(prog.gates.size(), 0);
     for (size_t g = 0; g < prog.gates.size(); ++g) {
         const PGate& G = prog.gates[g];
-        int s = G.offset;
+        int s = G.offset;  // half units
         for (auto& in : G.ins) {
             int v;
             if (in.src >= 0) {
@@ -468,10 +470,15 @@ int eval_program(const Program& prog, const uint8_t* content, size_t L) {
                 if (pos >= L) throw Error(FR_ERR_INVALID, "program references content past its end");
                 v = (content[pos] >> (2 * (cb % 4))) & 3;
             }
-            s += in.w * v;
+            s += 2 * in.w * v;
         }
-        if (s < 0 || s >= 16) throw Error(FR_ERR_INVALID, "program lincomb out of the 16-value message space");
-        val[g] = G.lut[s];
+        if (G.kind == GATE_SIGN) {
+            if ((s & 1) == 0 || s <= -32 || s >= 32) throw Error(FR_ERR_INVALID, "sign gate input out of (-16, 16) or integral");
+            val[g] = s > 0 ? 1 : 0;
+        } else {
+            if ((s & 1) || s < 0 || s >= 32) throw Error(FR_ERR_INVALID, "program lincomb out of the 16-value message space");
+            val[g] = G.lut[s / 2];
+        }
     }
     if (prog.out_gate < 0) return prog.out_const;
     return prog.out_const + prog.out_w * val[prog.out_gate];

@@ -1,10 +1,15 @@
 // Lowering of the recorded value DAG (what the reference computes through
 // tfhe-rs smart_* calls) into a program of programmable bootstraps (PBS).
 //
-// Every gate is  out = LUT( offset + sum_i w_i * in_i )  with the sum in
-// [0, 16) — one shortint-style PBS over a 16-value message space (Delta=2^59,
-// one padding bit).  Inputs are content blocks (2-bit radix digits of the
-// encrypted characters, src/regex/ciphertext.rs:18-29) or earlier gates.
+// Every gate is one programmable bootstrap of  s = offset/2 + sum_i w_i * in_i
+// (offset in units of Delta/2, Delta = 2^59).  Inputs are content blocks (2-bit
+// radix digits of the encrypted characters, src/regex/ciphertext.rs:18-29) or
+// earlier gates.  Two kinds:
+//  * LUT  : s integral in [0, 16), out = lut[s] (16-box test polynomial, one
+//           padding bit, as tfhe-rs shortint PARAM_MESSAGE_2_CARRY_2);
+//  * SIGN : s half-integral in (-16, 16), out = [s > 0] (constant test
+//           polynomial: the negacyclic rotation yields +-Delta/2, then +Delta/2).
+//           Threshold AND/OR of up to 16 literals in one bootstrap.
 //
 // FR_LOWER_FAITHFUL: one gate group per reference op (eq/gt/le = 3 PBS, and/or
 //   = 1 PBS, not = linear), the decomposition of SURVEY App. D.3.
@@ -25,9 +30,11 @@ struct PIn {
     int32_t src;  // >= 0: gate index; < 0: content block -(1 + pos*4 + blk)
     int32_t w;
 };
+enum GateKind : int32_t { GATE_LUT = 0, GATE_SIGN = 1 };
 struct PGate {
     std::vector<PIn> ins;
-    int32_t offset = 0;
+    int32_t offset = 0;  // units of Delta/2
+    int32_t kind = GATE_LUT;
     uint8_t lut[16] = {0};
     int32_t level = 0;
 };
@@ -39,7 +46,7 @@ struct Program {
     size_t max_width = 0;
 };
 
-constexpr int MAX_FANIN = 15;
+constexpr int MAX_FANIN = 16;
 
 Program lower(const ValueDag& dag, int root, int mode);
 // Plaintext semantics of a program (LUT semantics, with the [0,16) range

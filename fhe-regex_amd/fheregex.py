@@ -75,9 +75,13 @@ class PlainResult(C.Structure):
                 ("result_recorded", C.c_int32), ("result_lowered", C.c_int32)]
 
 
+GATE_LUT, GATE_SIGN = 0, 1
+
+
 class Gate(C.Structure):
-    _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("in_", C.c_uint32 * 15),
-                ("in_block", C.c_int8 * 15), ("in_w", C.c_int8 * 15), ("lut", C.c_uint8 * 16),
+    """fr_gate: offset in units of Delta/2; kind GATE_LUT or GATE_SIGN."""
+    _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("kind", C.c_int32), ("in_", C.c_uint32 * 16),
+                ("in_block", C.c_int8 * 16), ("in_w", C.c_int8 * 16), ("lut", C.c_uint8 * 16),
                 ("out", C.c_uint32)]
 
 

@@ -134,14 +134,19 @@ int fr_not(fr_ctx* ctx, fr_ct a, fr_ct* out);
 int fr_or_many(fr_ctx* ctx, const fr_ct* in, size_t n, fr_ct* out);
 
 /* ----- batched gate program ----- */
-/* One programmable bootstrap: out = PBS_lut(offset*Delta + sum_i w_i * in_i),
- * inputs are boolean/radix-block handles (block index in_block[i] of in[i]). */
+/* One programmable bootstrap of s = offset/2 + sum_i w_i * in_i (offset in
+ * units of Delta/2; inputs are boolean/radix-block handles, block in_block[i]
+ * of in[i]).  kind FR_GATE_LUT: s integral in [0,16), out = lut[s];
+ * kind FR_GATE_SIGN: s half-integral in (-16,16), out = [s > 0] (threshold
+ * AND/OR of up to 16 booleans). */
+enum { FR_GATE_LUT = 0, FR_GATE_SIGN = 1 };
 typedef struct {
     int32_t n_in;
     int32_t offset;
-    fr_ct in[15];
-    int8_t in_block[15];
-    int8_t in_w[15];
+    int32_t kind;
+    fr_ct in[16];
+    int8_t in_block[16];
+    int8_t in_w[16];
     uint8_t lut[16];
     fr_ct out; /* filled by fr_run_gates: a fresh boolean handle */
 } fr_gate;

@@ -218,8 +218,9 @@ class Oracle:
         return out
 
     def gates(self, gates, slots: np.ndarray) -> np.ndarray:
-        """gates: list of (inputs [(slot, weight)], offset, luts, direct) jobs; a
-        bare 16-entry lut means one direct output.  Returns all outputs, job-major."""
+        """gates: list of (inputs [(slot, weight)], offset, luts, direct) jobs, offset
+        in units of Delta/2; a bare 16-entry lut means one direct output; direct=2
+        is a sign gate (luts ignored).  Returns all outputs, job-major."""
         arr = (Gate * len(gates))()
         first = (C.c_int32 * len(gates))()
         total = 0
@@ -227,7 +228,7 @@ class Oracle:
             ins, off, luts = job[0], job[1], job[2]
             direct = job[3] if len(job) > 3 else None
             if len(luts) == 16 and not isinstance(luts[0], (list, tuple)):
-                luts, direct = [luts], True if direct is None else direct
+                luts, direct = [luts], 1 if direct is None else direct
             g = arr[q]
             g.n_in = len(ins)
             g.offset = off
@@ -235,7 +236,7 @@ class Oracle:
                 g.in_idx[t] = i
                 g.in_w[t] = w
             g.n_out = len(luts)
-            g.direct = int(bool(direct))
+            g.direct = int(direct or 0)
             for f, lut in enumerate(luts):
                 for t in range(16):
                     g.lut[f][t] = lut[t]

@@ -428,7 +428,9 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
     uint64_t* D = malloc(8 * kp1 * N);
     uint64_t* res = malloc(8 * N);
     uint64_t* V = malloc(8 * N);
-    if (direct) make_lut_poly(N, luts, V);
+    /* direct == 1: the LUT polynomial itself; 0 (multi-value) and 2 (sign gate):
+     * the constant test polynomial (Delta_p/2) * sum_j X^j */
+    if (direct == 1) make_lut_poly(N, luts, V);
     else for (int j = 0; j < N; j++) V[j] = DELTA_P / 2;
     uint32_t b = mod_switch(ks_lwe[n], log2N2);
     /* acc = (0, X^{-b} V) */
@@ -469,6 +471,7 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
         }
         const uint64_t* B = acc + (size_t)k * N;
         out[big] = or_conv(direct ? B[0] : apply_w(B, N, 0, nt, pos, d));
+        if (direct == 2) out[big] += 1ULL << 58; /* sign gate: +-Delta/2 + Delta/2 -> {0, Delta} */
     }
     free(acc); free(D); free(res); free(V);
 }
@@ -479,8 +482,9 @@ void or_blind_rotate(void* pk, const uint64_t* ks_lwe, const uint8_t lut[16], ui
 }
 
 /* ------------------------------------------------------------------ gates */
-/* A rotation job: c = offset*2^59 + sum_i w_i * in_i (mod 2^64), then one
- * blind rotation and n_out LUT outputs (factored unless direct). */
+/* A rotation job: c = offset*2^58 + sum_i w_i * in_i (mod 2^64), then one
+ * blind rotation and n_out LUT outputs (direct: 0 multi-value, 1 the LUT
+ * polynomial itself, 2 sign gate [c > 0]). */
 typedef struct {
     int32_t n_in;
     int32_t offset;
@@ -493,7 +497,7 @@ typedef struct {
 
 void or_lincomb(int big, const or_gate* g, const uint64_t* slots, uint64_t* out) {
     for (int t = 0; t <= big; t++) out[t] = 0;
-    out[big] = (uint64_t)(int64_t)g->offset << 59;
+    out[big] = (uint64_t)(int64_t)g->offset << 58;
     for (int q = 0; q < g->n_in; q++) {
         const uint64_t* x = slots + (size_t)g->in_idx[q] * (big + 1);
         uint64_t w = (uint64_t)(int64_t)g->in_w[q];

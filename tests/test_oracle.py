@@ -119,7 +119,7 @@ def test_oracle_pbs_lut(oracle_k1):
     blocks = O.encrypt_blocks(msgs, seed=21)
     blocks[3] = O.trivial_blocks([9])[0]
     luts = [[(3 * m + 1) % 16 for m in range(16)], [m ^ 1 for m in range(16)], list(range(16)), [1] * 16]
-    gates = [([(i, 1)], 0, luts[i]) for i in range(4)]
+    gates = [([(i, 1)], 0, luts[i]) for i in range(4)]  # offsets in units of Delta/2
     out = O.gates(gates, blocks)
     dec = O.decode16(out)
     assert [int(d) for d in dec] == [luts[i][msgs[i]] for i in range(4)]
@@ -153,3 +153,20 @@ def test_oracle_multi_value_bootstrap(oracle_k1):
                     else:
                         prod[k - N] -= d
         assert prod == V
+
+
+def test_oracle_sign_gate_fanin16(oracle_k1):
+    """Sign gates: OR/AND of 16 booleans in one bootstrap (offset in Delta/2 units)."""
+    O = oracle_k1
+    bits = [0] * 16
+    ct = O.encrypt_blocks(bits, seed=61)
+    ct1 = ct.copy()
+    ct1[9] = O.encrypt_blocks([1], seed=62)[0]
+    ones = O.encrypt_blocks([1] * 16, seed=63)
+    ins = [(i, 1) for i in range(16)]
+    jobs = [(ins, -1, [0] * 16, 2), (ins, 1 - 32, [0] * 16, 2)]  # OR: s - 1/2 ; AND: s - 16 + 1/2
+    out0 = O.gates(jobs, ct)
+    out1 = O.gates(jobs, ct1)
+    out2 = O.gates(jobs, ones)
+    dec = lambda o: [int(O.decode16(x)[0]) for x in o]
+    assert dec(out0) == [0, 0] and dec(out1) == [1, 0] and dec(out2) == [1, 1]
