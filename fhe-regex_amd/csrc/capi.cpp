@@ -10,6 +10,7 @@
 #include "device.h"
 #include "fheregex.h"
 #include "keys.h"
+#include "rns.h"
 #include "lower.h"
 #include "regex.h"
 
@@ -865,9 +866,9 @@ int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, 
 
 uint64_t fr_debug_scalar(int32_t op, uint64_t x, uint64_t y) {
     switch (op) {
-        case 0: return gl_mul(x, y);
-        case 1: return pbs_decompose(x);
-        case 2: return zp_to_torus(x);
+        case 0: return rns::crt((uint32_t)(x % rns::P0), (uint32_t)(x % rns::P1));
+        case 1: return (uint64_t)(int64_t)rns::decompose((uint32_t)(x % rns::P0), (uint32_t)(x % rns::P1));
+        case 2: return rns::to_torus((uint32_t)(x % rns::P0), (uint32_t)(x % rns::P1));
         case 3: return mod_switch(x, (int)y);
         case 4: {
             int32_t d[5];

@@ -46,7 +46,7 @@ class Device {
     const Params& params() const { return p_; }
     int device() const { return dev_; }
 
-    // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod P [i][r][c][coef]
+    // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod Q [i][r][c][coef]
     void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
     bool has_keys() const { return d_ksk_ && d_bsk_; }
 
@@ -85,13 +85,13 @@ class Device {
 
     Params p_;
     int dev_;
-    int e_ = 8;        // coefficients per lane in the NTT kernels (4 or 8)
-    int e_small_ = 4;  // ... for launches of at most small_batch_ bootstraps
+    int e_ = 16;       // residues per lane in the NTT kernels (8 or 16)
+    int e_small_ = 8;  // ... for launches of at most small_batch_ bootstraps
     size_t small_batch_ = 256;
     void* stream_ = nullptr;  // hipStream_t
     uint64_t* d_ksk_ = nullptr;
-    uint64_t* d_bsk_ = nullptr;  // NTT domain, scaled by 1/N
-    uint64_t* d_tw_ = nullptr;   // zeta[N], izeta[N]
+    uint32_t* d_bsk_ = nullptr;  // NTT domain [i][r][c][prime][slot], Montgomery form, scaled by 1/N
+    uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
     uint64_t* d_arena_ = nullptr;
     size_t arena_cap_ = 0;
     std::vector<int> free_slots_;

@@ -2,33 +2,36 @@
 //
 //   k_lincomb_keyswitch : lincomb of input LWEs (mod 2^64) fused with the
 //                         LWE keyswitch kN -> n (signed base 2^3, 5 levels)
-//   k_blind_rotate<N,K> : modulus switch, LUT accumulator, n CMUX steps
-//                         (rotate -> gadget decompose -> forward NTT -> MAC with
-//                         the NTT-domain GGSW -> inverse NTT -> accumulate),
-//                         sample extract, Z_p -> 2^64 conversion.
-//                         One workgroup of (K+1)*N/16 threads per bootstrap:
-//                         each polynomial is owned by N/16 lanes holding 16
-//                         coefficients in registers; the 11 NTT stages run as
-//                         3 register-resident phases (4+4+3 stages) joined by
-//                         two LDS exchanges.
-//   k_bsk_to_ntt<N,K>   : one-time forward NTT of the bootstrapping key.
+//   k_blind_rotate<N,K,E>: modulus switch, test-polynomial accumulator, n CMUX
+//                         steps (rotate -> gadget decompose -> forward NTT ->
+//                         MAC with the NTT-domain GGSW -> inverse NTT ->
+//                         accumulate), multi-value w-step, sample extract,
+//                         Z_Q -> 2^64 conversion.
+//   k_bsk_to_ntt<N,K,E> : one-time forward NTT of the bootstrapping key.
 //
-// Arithmetic: Goldilocks prime P = 2^64 - 2^32 + 1 (common.h), 64x64->128 via
-// four v_mad_u64_u32, reduction with shifts/adds only.  The NTT is the
-// merged-psi negacyclic Cooley-Tukey (forward) / Gentleman-Sande (inverse)
-// transform: zeta[k] = psi^brv(k); outputs in bit-reversed slot order.
+// Ring: Z_Q[X]/(X^N+1), Q = p0*p1 (rns.h), two 30-bit NTT primes.  One
+// workgroup per bootstrap with 2*(K+1)*N/E lanes: each (polynomial, prime)
+// pair is owned by N/E lanes (whole waves) holding E residues in registers.
+// The log2 N NTT stages run as register-resident phases of log2 E stages
+// joined by LDS exchanges.  Butterflies are Harvey-lazy with Montgomery
+// products (R = 2^32): forward values stay in [0, 4p), inverse in [0, 2p),
+// 32-bit adds and v_min_u32 only.  Twiddles and the BSK are in Montgomery
+// form (1/N folded into the BSK); data is in normal form.  The merged-psi
+// negacyclic transform: forward Cooley-Tukey with zeta[k] = psi^brv(k),
+// outputs in bit-reversed slot order; inverse Gentleman-Sande with
+// psi^-brv(k) = -zeta[3*2^s - 1 - k] (negation folded into the butterfly).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
-#include <type_traits>
 #include <cstring>
 #include <sstream>
+#include <type_traits>
 
 #include "device.h"
-#include "gl_device.h"
 #include "keys.h"
+#include "rns.h"
 
 namespace fr {
 
@@ -40,335 +43,435 @@ namespace fr {
                                         " at " __FILE__ ":" + std::to_string(__LINE__));     \
     } while (0)
 
+using rns::mont;
+using rns::mont_lazy;
+using rns::red1;
+using rns::red2;
+
 // ------------------------------------------------------------------ geometry
 constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
+
+// one padding word per 16 (conflict-free strided phases)
+__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
 
 // N-point negacyclic NTT spread over T = N/E lanes holding E coefficients
 // each.  The LOG = log2 N stages run as NPH register-resident phases of e =
 // log2 E stages; phase p's lane owns the E elements that differ in index bits
 // [lo(p), lo(p)+e), and two consecutive phases are joined by one LDS
-// exchange.  Forward stage s pairs bit LOG-1-s with zeta[(1<<s) + (j >> (LOG-s))],
-// zeta[k] = psi^brv(k); the inverse uses psi^-brv(k) = -zeta[3*2^s - 1 - k].
+// exchange.  Forward stage s pairs bit LOG-1-s with zeta[(1<<s) + (j >> (LOG-s))].
 template <int N, int E>
 struct NttGeo {
     static constexpr int LOG = ilog2c(N);
     static constexpr int e = ilog2c(E);
     static constexpr int T = N / E;
     static constexpr int NPH = (LOG + e - 1) / e;
-    static constexpr int NP = N + N / 16;  // padded LDS row (u64)
+    static constexpr int NP = N + N / 16;  // padded LDS row (u32)
     static_assert((1 << LOG) == N && (1 << e) == E, "powers of two");
+    static_assert(T % 64 == 0, "a (polynomial, prime) pair must own whole waves");
     static constexpr int lo(int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
     static constexpr int s_begin(int p) { return p * e; }
     static constexpr int s_end(int p) { return (p + 1) * e < LOG ? (p + 1) * e : LOG; }
-    __device__ static __forceinline__ int pad(int i) { return i + (i >> 4); }
+    __device__ static __forceinline__ int pad(int i) { return lds_pad(i); }
+    // element m of lane tl in phase p: idx = base(tl) | moff(m), disjoint bits,
+    // so pad(idx) = pad(base) + pad(moff) and x >> k splits the same way: every
+    // address is one per-lane register plus a compile-time immediate.
     template <int p>
-    __device__ static __forceinline__ int idx(int tl, int m) {
+    __device__ static __forceinline__ int base(int tl) {
         constexpr int L = lo(p);
-        return ((tl >> L) << (L + e)) | (m << L) | (tl & ((1 << L) - 1));
+        return ((tl >> L) << (L + e)) | (tl & ((1 << L) - 1));
     }
+    template <int p>
+    static constexpr int moff(int m) { return m << lo(p); }
+    template <int p>
+    __device__ static __forceinline__ int idx(int tl, int m) { return base<p>(tl) + moff<p>(m); }
 };
+constexpr int pad_c(int i) { return i + (i >> 4); }
+
+// Montgomery product a*b/2^32 in [0, 2p) (a*b < 4p^2).  (No inline asm in
+// this file: the waitcnt pass drains every outstanding load before one.)
+__device__ __forceinline__ uint32_t mont_lazy_d(uint32_t a, uint32_t b, uint32_t p, uint32_t pn) {
+    return mont_lazy(a, b, p, pn);
+}
+
+// Harvey-lazy Cooley-Tukey butterfly: x, y in [0, 4p) -> [0, 4p); w Montgomery
+__device__ __forceinline__ void ct_lazy(uint32_t& x, uint32_t& y, uint32_t w, uint32_t p, uint32_t pn) {
+    x = red2(x, p);
+    const uint32_t t = mont_lazy_d(y, w, p, pn);  // [0, 2p)
+    y = x - t + 2 * p;
+    x = x + t;
+}
+// Gentleman-Sande with the flipped twiddle w = -psi^-brv(k):
+// (u, v) -> (u + v, (v - u) * w), values in [0, 2p)
+__device__ __forceinline__ void gs_lazy(uint32_t& u, uint32_t& v, uint32_t w, uint32_t p, uint32_t pn) {
+    const uint32_t s = red2(u + v, p);
+    const uint32_t d = v - u + 2 * p;  // (0, 4p)
+    v = mont_lazy_d(d, w, p, pn);
+    u = s;
+}
 
 template <int N, int E, int p>
-__device__ __forceinline__ void fwd_phase(uint64_t (&x)[E], const uint64_t* zt, int tl) {
+__device__ __forceinline__ void fwd_phase(uint32_t (&x)[E], const uint32_t* zt, int tl, uint32_t pm, uint32_t pn) {
     using G = NttGeo<N, E>;
+    const int b = G::template base<p>(tl);
 #pragma unroll
     for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
         const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+        const uint32_t* zs = zt + (b >> (G::LOG - s));
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             if (m & dm) continue;
-            const int j = G::template idx<p>(tl, m);
-            gd::ct(x[m], x[m + dm], zt[(1 << s) + (j >> (G::LOG - s))]);
+            ct_lazy(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))], pm, pn);
         }
     }
 }
 template <int N, int E, int p>
-__device__ __forceinline__ void inv_phase(uint64_t (&x)[E], const uint64_t* zt, int tl) {
+__device__ __forceinline__ void inv_phase(uint32_t (&x)[E], const uint32_t* zt, int tl, uint32_t pm, uint32_t pn) {
     using G = NttGeo<N, E>;
+    const int b = G::template base<p>(tl);
 #pragma unroll
     for (int s = G::s_end(p) - 1; s >= G::s_begin(p); --s) {
         const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+        // zt[3*2^s - 1 - k], k = 2^s + (j >> (LOG-s))
+        const uint32_t* zs = zt - (b >> (G::LOG - s));
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             if (m & dm) continue;
-            const int j = G::template idx<p>(tl, m);
-            const int k = (1 << s) + (j >> (G::LOG - s));
-            gd::gs(x[m], x[m + dm], zt[3 * (1 << s) - 1 - k]);
+            gs_lazy(x[m], x[m + dm], zs[2 * (1 << s) - 1 - (G::template moff<p>(m) >> (G::LOG - s))], pm, pn);
         }
     }
 }
 // LDS exchange between the layouts of phases PF and PT (row = this lane's polynomial)
 template <int N, int E, int PF, int PT>
-__device__ __forceinline__ void exchange(uint64_t (&x)[E], uint64_t* row, int tl) {
+__device__ __forceinline__ void exchange(uint32_t (&x)[E], uint32_t* row, int tl) {
     using G = NttGeo<N, E>;
+    uint32_t* rf = row + G::pad(G::template base<PF>(tl));
+    uint32_t* rt = row + G::pad(G::template base<PT>(tl));
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<PF>(tl, m))] = x[m];
+    for (int m = 0; m < E; ++m) rf[pad_c(G::template moff<PF>(m))] = x[m];
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) x[m] = row[G::pad(G::template idx<PT>(tl, m))];
+    for (int m = 0; m < E; ++m) x[m] = rt[pad_c(G::template moff<PT>(m))];
 }
 
 template <int N, int E, int p>
-__device__ __forceinline__ void forward_from(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
-    fwd_phase<N, E, p>(x, zt, tl);
+__device__ __forceinline__ void forward_from(uint32_t (&x)[E], uint32_t* row, const uint32_t* zt, int tl, uint32_t pm,
+                                             uint32_t pn) {
+    fwd_phase<N, E, p>(x, zt, tl, pm, pn);
     if constexpr (p + 1 < NttGeo<N, E>::NPH) {
         exchange<N, E, p, p + 1>(x, row, tl);
-        forward_from<N, E, p + 1>(x, row, zt, tl);
+        forward_from<N, E, p + 1>(x, row, zt, tl, pm, pn);
     }
 }
 template <int N, int E, int p>
-__device__ __forceinline__ void inverse_from(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
-    inv_phase<N, E, p>(x, zt, tl);
+__device__ __forceinline__ void inverse_from(uint32_t (&x)[E], uint32_t* row, const uint32_t* zt, int tl, uint32_t pm,
+                                             uint32_t pn) {
+    inv_phase<N, E, p>(x, zt, tl, pm, pn);
     if constexpr (p > 0) {
         exchange<N, E, p, p - 1>(x, row, tl);
-        inverse_from<N, E, p - 1>(x, row, zt, tl);
+        inverse_from<N, E, p - 1>(x, row, zt, tl, pm, pn);
     }
 }
-// natural order (phase-0 layout) -> bit-reversed slots (last-phase layout)
+// natural order (phase-0 layout), values < 4p -> bit-reversed slots (last-phase layout), < 4p
 template <int N, int E>
-__device__ __forceinline__ void forward_ntt(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
-    forward_from<N, E, 0>(x, row, zt, tl);
+__device__ __forceinline__ void forward_ntt(uint32_t (&x)[E], uint32_t* row, const uint32_t* zt, int tl, uint32_t pm,
+                                            uint32_t pn) {
+    forward_from<N, E, 0>(x, row, zt, tl, pm, pn);
 }
-// last-phase layout -> natural order, without the 1/N factor
+// last-phase layout, values < 2p -> natural order, < 2p; without the 1/N factor
 template <int N, int E>
-__device__ __forceinline__ void inverse_ntt(uint64_t (&x)[E], uint64_t* row, const uint64_t* zt, int tl) {
-    inverse_from<N, E, NttGeo<N, E>::NPH - 1>(x, row, zt, tl);
+__device__ __forceinline__ void inverse_ntt(uint32_t (&x)[E], uint32_t* row, const uint32_t* zt, int tl, uint32_t pm,
+                                            uint32_t pn) {
+    inverse_from<N, E, NttGeo<N, E>::NPH - 1>(x, row, zt, tl, pm, pn);
 }
 
 // ------------------------------------------------------------ blind rotation
 template <int N, int K, int E>
-constexpr size_t br_smem_bytes() {
-    return sizeof(uint64_t) * ((size_t)(K + 1) * NttGeo<N, E>::NP + (size_t)N) + 16 * MAX_OUT + 2 * 1024;
+constexpr int br_threads() {
+    return 2 * (K + 1) * (N / E);
 }
 template <int N, int K, int E>
-constexpr int br_threads() {
-    return (K + 1) * (N / E);
+constexpr size_t br_smem_bytes() {
+    return sizeof(uint32_t) * (2 * (size_t)(K + 1) * NttGeo<N, E>::NP + 2 * (size_t)N) + 16 * MAX_OUT + 2 * 1024;
 }
 
-// BSK NTT-domain layout: natural (bit-reversed) slot order, the same for every
-// lane geometry E, so the lane count can be chosen per launch.
+// BSK NTT-domain layout [i][r][c][prime][slot]: natural (bit-reversed) slot
+// order, the same for every lane geometry E, so E can be chosen per launch.
 template <int N, int E>
 __device__ __forceinline__ int bsk_pos(int tl, int m) {
     return NttGeo<N, E>::template idx<NttGeo<N, E>::NPH - 1>(tl, m);
 }
 
-// minimum waves per SIMD: E=8 caps registers at 128 so two 512-thread
-// workgroups share a CU (measured +27% saturated throughput over 146 VGPRs)
+// minimum waves per SIMD (register cap 512 / w): 4 -> 128 VGPRs
+#ifndef FR_BR_MINW8
+#define FR_BR_MINW8 4
+#endif
+#ifndef FR_BR_MINW16
+#define FR_BR_MINW16 4
+#endif
 template <int E>
 constexpr int br_min_waves() {
-    return E == 8 ? 4 : E == 4 ? 4 : 1;
+    return E == 16 ? FR_BR_MINW16 : FR_BR_MINW8;
 }
+
+// (x_0, x_1) residues of sum_t d_t (X^pos_t A)[j] for the multi-value w-step
+template <int N>
+__device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint8_t* lf, int j, uint32_t pm, int q) {
+    constexpr int box = N / 16, half = box / 2;
+    uint64_t pos = 0, neg = 0;
+    for (int tt = 1; tt <= 16; ++tt) {
+        int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+        if (d == 0) continue;  // uniform across the workgroup
+        int src = j - (tt < 16 ? tt * box - half : N - half);
+        if (src < 0) {
+            src += N;
+            d = -d;
+        }
+        const uint64_t v = row[lds_pad(src)];
+        if (d > 0) pos += v * (uint64_t)d;
+        else neg += v * (uint64_t)(-d);
+    }
+    // |sum| < 16 * 30 * p: shift by 512p before reducing
+    return rns::reduce64(pos + 512ULL * pm - neg, q);
+}
+
 template <int N, int K, int E>
-__global__ void __launch_bounds__((K + 1) * (N / E), br_min_waves<E>())
+__global__ void __launch_bounds__(2 * (K + 1) * (N / E), br_min_waves<E>())
 k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
-               const uint64_t* __restrict__ bsk, const uint64_t* __restrict__ tw, uint64_t* __restrict__ arena,
+               const uint32_t* __restrict__ bsk, const uint32_t* __restrict__ tw, uint64_t* __restrict__ arena,
                int slot_stride) {
     using G = NttGeo<N, E>;
     constexpr int NT = br_threads<N, K, E>();
     constexpr int LAST = G::NPH - 1;
-    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    uint64_t* xbuf = smem;                   // (K+1) rows of NP
-    uint64_t* zt = xbuf + (K + 1) * G::NP;   // N
-    uint8_t* lut = (uint8_t*)(zt + N);                // 16 * n_out
-    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024)
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* xbuf = smem;                                // 2(K+1) rows of NP: row (P, q) at (2P + q) * NP
+    uint32_t* zt_all = xbuf + 2 * (K + 1) * G::NP;       // 2 x N Montgomery twiddles
+    uint8_t* lut = (uint8_t*)(zt_all + 2 * N);           // 16 * n_out
+    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);    // n (<= 1024)
 
     const int tid = threadIdx.x;
-    const int P = tid / G::T, tl = tid % G::T;
+    const int PQ = __builtin_amdgcn_readfirstlane(tid / G::T), tl = tid % G::T;  // wave-uniform
+    const int P = PQ >> 1, q = PQ & 1;
+    const uint32_t pm = rns::prime(q), pn = rns::pneg(q);
     const int g = blockIdx.x;
     const uint64_t* in = ks + (size_t)g * ks_stride;
 
     const int n_out = gates[g].n_out;
     const int kind = gates[g].direct;
     const bool direct = kind == JOB_DIRECT;
-    for (int i = tid; i < N; i += NT) zt[i] = tw[i];
+    for (int i = tid; i < 2 * N; i += NT) zt_all[i] = tw[i];
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
     const uint32_t bbar = mod_switch(in[n], G::LOG + 1);
     __syncthreads();
+    const uint32_t* zt = zt_all + q * N;
 
-    uint64_t* row = xbuf + P * G::NP;
-    uint64_t acc[E];  // canonical, natural order: coefficient idx<0>(tl, m)
+    uint32_t* row = xbuf + PQ * G::NP;
+    const uint32_t* row0 = xbuf + (2 * P) * G::NP;  // this polynomial, prime 0
+    const uint32_t* row1 = row0 + G::NP;            // ... prime 1
+    const int b0 = G::template base<0>(tl), bl = G::template base<LAST>(tl);
+    uint32_t* row_b0 = row + G::pad(b0);
+    const uint32_t* row0_b0 = row0 + G::pad(b0);
+    const uint32_t* row1_b0 = row1 + G::pad(b0);
+    uint32_t* row_bl = row + G::pad(bl);
+    const uint32_t* xbuf_q_bl = xbuf + q * G::NP + G::pad(bl);
+    uint32_t acc[E];  // canonical residues, natural order: coefficient idx<0>(tl, m)
     {
+        // acc = (0, X^-bbar * V): V's residues into the body rows, then rotate
         constexpr int box = N / 16, half = box / 2;
+        if (P == K) {
+            const uint32_t dqr = q ? rns::DQR1 : rns::DQR0;
+            const uint32_t hq = q ? rns::HQ1 : rns::HQ0;
+            for (int jj = tl; jj < N; jj += G::T) {
+                uint32_t v = hq;  // multi-value / sign test polynomial (Delta/2) * u
+                if (direct) {
+                    const int mm = (jj + half) / box;
+                    v = mm < 16 ? mont(lut[mm], dqr, pm, pn) : rns::negm(mont(lut[0], dqr, pm, pn), pm);
+                }
+                row[G::pad(jj)] = v;
+            }
+        }
+        __syncthreads();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             acc[m] = 0;
             if (P == K) {
-                const int s = (G::template idx<0>(tl, m) + (int)bbar) & (2 * N - 1);
-                const int sp = s < N ? s : s - N;
-                const int mm = (sp + half) / box;
-                uint64_t v = DELTA_P / 2;  // multi-value test polynomial (Delta/2) * u
-                if (direct) v = mm < 16 ? (uint64_t)lut[mm] * DELTA_P : gl_neg((uint64_t)lut[0] * DELTA_P);
-                acc[m] = s < N ? v : gl_neg(v);
+                const int s = (b0 + G::template moff<0>(m) + (int)bbar) & (2 * N - 1);
+                const uint32_t v = row[G::pad(s & (N - 1))];
+                acc[m] = s < N ? v : rns::negm(v, pm);
             }
         }
     }
 
-    const size_t ggsw = (size_t)(K + 1) * (K + 1) * N;
+    const size_t ggsw = (size_t)(K + 1) * (K + 1) * 2 * N;
     for (int i = 0; i < n; ++i) {
         const int a = abar[i];
         if (a == 0) continue;  // X^0*acc - acc = 0: exact no-op (uniform branch)
-        // 1. rotate (X^a - 1) * acc and decompose
-        uint64_t x[E];
-        __syncthreads();
+        // 0. prefetch this lane's GGSW_i slots; they land during steps 1-2
+        //    (__syncthreads only drains LDS counters, not these loads)
+        uint32_t gv[K + 1][E];
+        {
+            const uint32_t* gi = bsk + (size_t)i * ggsw + (size_t)(P * 2 + q) * N + bl;
 #pragma unroll
-        for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = acc[m];
-        __syncthreads();
+            for (int r = 0; r <= K; ++r)
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int s = (G::template idx<0>(tl, m) - a) & (2 * N - 1);
-            const uint64_t v = s < N ? row[G::pad(s)] : gl_neg(row[G::pad(s - N)]);
-            x[m] = pbs_decompose(gl_sub(v, acc[m]));
+                for (int m = 0; m < E; ++m) gv[r][m] = gi[(size_t)r * (K + 1) * 2 * N + G::template moff<LAST>(m)];
         }
-        // 2. forward NTT of this lane group's digit polynomial
-        forward_ntt<N, E>(x, row, zt, tl);
-        // 3. external product MAC (in place): x_P = sum_r D_r * GGSW_i[r][P]
+        // 1. (X^a - 1) * acc, CRT of the two residues, signed gadget digit
+        uint32_t x[E];
         __syncthreads();
 #pragma unroll
-        for (int m = 0; m < E; ++m) row[G::pad(G::template idx<LAST>(tl, m))] = x[m];
+        for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
         __syncthreads();
-        const uint64_t* gi = bsk + (size_t)i * ggsw;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const int pos = G::pad(G::template idx<LAST>(tl, m));
-            uint64_t sacc = 0;
+            const int j = b0 + G::template moff<0>(m);
+            const int s = (j - a) & (2 * N - 1);
+            const int sp = G::pad(s < N ? s : s - N);
+            uint32_t v0 = row0[sp], v1 = row1[sp];
+            if (s >= N) {
+                v0 = rns::negm(v0, rns::P0);
+                v1 = rns::negm(v1, rns::P1);
+            }
+            const int jo = pad_c(G::template moff<0>(m));
+            const int32_t dg = rns::decompose(rns::subm(v0, row0_b0[jo], rns::P0), rns::subm(v1, row1_b0[jo], rns::P1));
+            x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
+        }
+        // 2. forward NTT of this lane group's digit residues
+        forward_ntt<N, E>(x, row, zt, tl, pm, pn);
+        // 3. external product MAC (in place): x_(P,q) = sum_r D_(r,q) * GGSW_i[r][P][q]
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int po = pad_c(G::template moff<LAST>(m));
+            uint32_t sacc = 0;
 #pragma unroll
             for (int r = 0; r <= K; ++r) {
-                const uint64_t d = (r == P) ? x[m] : xbuf[r * G::NP + pos];
-                const uint64_t gv = gi[((size_t)(r * (K + 1) + P)) * N + bsk_pos<N, E>(tl, m)];
-                sacc = r == 0 ? gd::mul(d, gv) : gd::add_g(sacc, gd::mul(d, gv));
+                const uint32_t d = (r == P) ? x[m] : xbuf_q_bl[2 * r * G::NP + po];
+                sacc = red2(sacc + mont_lazy_d(d, gv[r][m], pm, pn), pm);
             }
-            x[m] = sacc;
+            x[m] = sacc;  // [0, 2p)
         }
         // 4. inverse NTT and accumulate (1/N is folded into the BSK)
-        inverse_ntt<N, E>(x, row, zt, tl);
+        inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
 #pragma unroll
-        for (int m = 0; m < E; ++m) acc[m] = gd::canon(gd::add_c(x[m], acc[m]));
+        for (int m = 0; m < E; ++m) acc[m] = red1(red1(x[m], pm) + acc[m], pm);
     }
 
-    // sample extract (coefficient 0) under the flattened key, then Z_p -> 2^64
+    // publish the accumulator: the outputs need both residues of a coefficient
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
+    __syncthreads();
+    const int big = K * N;
     if (kind != JOB_MULTI) {
+        // sample extract (coefficient 0) under the flattened key, then Z_Q -> 2^64
         uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
         // sign gate: +-Delta/2 (+ Delta/2) -> {0, Delta}
         const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int j = G::template idx<0>(tl, m);
-            if (P < K) {
-                const int t = j == 0 ? 0 : N - j;
-                const uint64_t v = j == 0 ? acc[m] : gl_neg(acc[m]);
-                out[P * N + t] = zp_to_torus(v);
-            } else if (j == 0) {
-                out[K * N] = zp_to_torus(acc[m]) + post;
+        for (int c = tid; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint32_t* r0 = xbuf + 2 * pp * G::NP;
+            uint32_t v0 = r0[G::pad(j)], v1 = r0[G::NP + G::pad(j)];
+            if (t != 0) {
+                v0 = rns::negm(v0, rns::P0);
+                v1 = rns::negm(v1, rns::P1);
             }
+            out[c] = rns::to_torus(v0, v1) + (c == big ? post : 0);
         }
         return;
     }
     // multi-value: acc_f = w_f * acc with w_f = sum_t d_t X^{pos_t} (small d_t)
-    __syncthreads();
-#pragma unroll
-    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = acc[m];
-    __syncthreads();
-    constexpr int box = N / 16, half = box / 2;
     for (int f = 0; f < n_out; ++f) {
         const uint8_t* lf = lut + 16 * f;
         uint64_t* out = arena + (size_t)gates[g].out_slot[f] * slot_stride;
-#pragma unroll
-        for (int m = 0; m < E; ++m) {
-            const int j = G::template idx<0>(tl, m);
-            if (P == K && j != 0) continue;
-            // positive / negative parts of sum_t d_t * (X^pos_t A)[j], limb-split (< 2^42 each)
-            uint64_t pl = 0, ph = 0, nl = 0, nh = 0;
-            for (int tt = 1; tt <= 16; ++tt) {
-                int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
-                if (d == 0) continue;  // uniform across the workgroup
-                const int pos = tt < 16 ? tt * box - half : N - half;
-                int src = j - pos;
-                if (src < 0) {
-                    src += N;
-                    d = -d;
-                }
-                const uint64_t v = row[G::pad(src)];
-                const uint64_t ad = (uint64_t)(d < 0 ? -d : d);
-                const uint64_t lo = (v & 0xFFFFFFFFULL) * ad, hi = (v >> 32) * ad;
-                if (d > 0) { pl += lo; ph += hi; } else { nl += lo; nh += hi; }
+        for (int c = tid; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint32_t* r0 = xbuf + 2 * pp * G::NP;
+            uint32_t v0 = w_step<N>(r0, lf, j, rns::P0, 0), v1 = w_step<N>(r0 + G::NP, lf, j, rns::P1, 1);
+            if (t != 0) {
+                v0 = rns::negm(v0, rns::P0);
+                v1 = rns::negm(v1, rns::P1);
             }
-            // value = (ph - nh) * 2^32 + (pl - nl)  (mod P)
-            const int64_t A = (int64_t)(pl - nl), Bv = (int64_t)(ph - nh);
-            const int64_t B1 = Bv >> 32;
-            const uint64_t B0 = (uint64_t)Bv & 0xFFFFFFFFULL;
-            const int64_t Cv = A + B1 * (int64_t)4294967296LL - B1;  // + B1 * (2^32 - 1)
-            const uint64_t u = B0 << 32;
-            uint64_t r = u + (uint64_t)Cv;
-            if (Cv >= 0 && r < u) r += EPS;
-            if (Cv < 0 && u < (uint64_t)(-Cv)) r -= EPS;
-            r = gd::canon(r);
-            if (P < K) {
-                const int t = j == 0 ? 0 : N - j;
-                out[P * N + t] = zp_to_torus(j == 0 ? r : gl_neg(r));
-            } else {
-                out[K * N] = zp_to_torus(r);
-            }
+            out[c] = rns::to_torus(v0, v1);
         }
     }
 }
 
 // ------------------------------------------------------ BSK -> NTT domain
+// block = (i, r); lanes (c, prime): residue of the mod-Q coefficient, to
+// Montgomery form, forward NTT, canonical, times 1/N.
 template <int N, int K, int E>
-__global__ void __launch_bounds__((K + 1) * (N / E))
-k_bsk_to_ntt(const uint64_t* __restrict__ coef, const uint64_t* __restrict__ tw, uint64_t n_inv,
-             uint64_t* __restrict__ out) {
+__global__ void __launch_bounds__(2 * (K + 1) * (N / E))
+k_bsk_to_ntt(const uint64_t* __restrict__ coef, const uint32_t* __restrict__ tw, uint32_t ninv_r0, uint32_t ninv_r1,
+             uint32_t* __restrict__ out) {
     using G = NttGeo<N, E>;
     constexpr int NT = br_threads<N, K, E>();
-    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    uint64_t* xbuf = smem;
-    uint64_t* zt = xbuf + (K + 1) * G::NP;
-    const int tid = threadIdx.x, P = tid / G::T, tl = tid % G::T;
-    for (int i = tid; i < N; i += NT) zt[i] = tw[i];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* xbuf = smem;
+    uint32_t* zt_all = xbuf + 2 * (K + 1) * G::NP;
+    const int tid = threadIdx.x, PQ = __builtin_amdgcn_readfirstlane(tid / G::T), tl = tid % G::T;
+    const int P = PQ >> 1, q = PQ & 1;
+    const uint32_t pm = rns::prime(q), pn = rns::pneg(q);
+    const uint32_t r2 = q ? rns::R2_1 : rns::R2_0, ninv = q ? ninv_r1 : ninv_r0;
+    for (int i = tid; i < 2 * N; i += NT) zt_all[i] = tw[i];
     __syncthreads();
-    const size_t poly = ((size_t)blockIdx.x * (K + 1) + P) * N;  // blockIdx.x = i*(K+1) + r
-    uint64_t x[E];
+    const size_t poly = (size_t)blockIdx.x * (K + 1) + P;  // blockIdx.x = i*(K+1) + r
+    uint32_t x[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) x[m] = coef[poly + G::template idx<0>(tl, m)];
-    forward_ntt<N, E>(x, xbuf + P * G::NP, zt, tl);
+    for (int m = 0; m < E; ++m) x[m] = mont(rns::reduce64(coef[poly * N + G::template idx<0>(tl, m)], q), r2, pm, pn);
+    forward_ntt<N, E>(x, xbuf + PQ * G::NP, zt_all + q * N, tl, pm, pn);
 #pragma unroll
-    for (int m = 0; m < E; ++m) out[poly + bsk_pos<N, E>(tl, m)] = gl_mul(gd::canon(x[m]), n_inv);
+    for (int m = 0; m < E; ++m) out[(poly * 2 + q) * N + bsk_pos<N, E>(tl, m)] = mont(red1(red2(x[m], pm), pm), ninv, pm, pn);
 }
 
 // ------------------------------------------------ ring product (parity test)
+// lanes (operand, prime); product of a, b in [0, Q) mod Q
 template <int N, int E>
-__global__ void __launch_bounds__(2 * (N / E))
-k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const uint64_t* __restrict__ tw,
-           uint64_t n_inv, uint64_t* __restrict__ out) {
+__global__ void __launch_bounds__(4 * (N / E))
+k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const uint32_t* __restrict__ tw,
+           uint32_t r2n0, uint32_t r2n1, uint64_t* __restrict__ out) {
     using G = NttGeo<N, E>;
     constexpr int LAST = G::NPH - 1;
-    extern __shared__ __attribute__((aligned(16))) uint64_t smem[];
-    uint64_t* xbuf = smem;
-    uint64_t* zt = xbuf + 2 * G::NP;
-    const int tid = threadIdx.x, P = tid / G::T, tl = tid % G::T;
-    for (int i = tid; i < N; i += 2 * G::T) zt[i] = tw[i];
+    extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
+    uint32_t* xbuf = smem;  // rows (operand, prime)
+    uint32_t* zt_all = xbuf + 4 * G::NP;
+    const int tid = threadIdx.x, PQ = __builtin_amdgcn_readfirstlane(tid / G::T), tl = tid % G::T;
+    const int P = PQ >> 1, q = PQ & 1;
+    const uint32_t pm = rns::prime(q), pn = rns::pneg(q);
+    for (int i = tid; i < 2 * N; i += 4 * G::T) zt_all[i] = tw[i];
     __syncthreads();
+    const uint32_t* zt = zt_all + q * N;
     const uint64_t* src = (P == 0 ? a : b) + (size_t)blockIdx.x * N;
-    uint64_t x[E];
+    uint32_t x[E];
 #pragma unroll
-    for (int m = 0; m < E; ++m) x[m] = src[G::template idx<0>(tl, m)];
-    uint64_t* row = xbuf + P * G::NP;
-    forward_ntt<N, E>(x, row, zt, tl);
+    for (int m = 0; m < E; ++m) x[m] = rns::reduce64(src[G::template idx<0>(tl, m)], q);
+    uint32_t* row = xbuf + PQ * G::NP;
+    forward_ntt<N, E>(x, row, zt, tl, pm, pn);
     __syncthreads();
 #pragma unroll
     for (int m = 0; m < E; ++m) row[G::pad(G::template idx<LAST>(tl, m))] = x[m];
     __syncthreads();
+    // a*b/R, then * R^2/N / R
+    const uint32_t r2n = q ? r2n1 : r2n0;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int pos = G::pad(G::template idx<LAST>(tl, m));
-        x[m] = gd::mul(gd::mul(xbuf[pos], xbuf[G::NP + pos]), n_inv);
+        const uint32_t u = red1(red2(xbuf[q * G::NP + pos], pm), pm);  // operand a, canonical
+        x[m] = mont(mont_lazy(u, xbuf[(2 + q) * G::NP + pos], pm, pn), r2n, pm, pn);
     }
-    inverse_ntt<N, E>(x, row, zt, tl);
-    if (P == 0) {
+    inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
+    __syncthreads();
 #pragma unroll
-        for (int m = 0; m < E; ++m) out[(size_t)blockIdx.x * N + G::template idx<0>(tl, m)] = gd::canon(x[m]);
-    }
+    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = red1(x[m], pm);
+    __syncthreads();
+    for (int c = tid; c < N; c += 4 * G::T)
+        out[(size_t)blockIdx.x * N + c] = rns::crt(xbuf[G::pad(c)], xbuf[G::NP + G::pad(c)]);
 }
 
 // ------------------------------------------------- lincomb + keyswitch
@@ -491,11 +594,11 @@ static void dispatch(const Params& p, int E, F&& body) {
     using I1024 = std::integral_constant<int, 1024>;
     using I1 = std::integral_constant<int, 1>;
     using I2 = std::integral_constant<int, 2>;
-    using E4 = std::integral_constant<int, 4>;
     using E8 = std::integral_constant<int, 8>;
-    if (pick(I2048{}, I1{}, E8{}) || pick(I2048{}, I1{}, E4{})) return;
-    if (pick(I1024{}, I2{}, E8{}) || pick(I1024{}, I2{}, E4{})) return;
-    if (pick(I1024{}, I1{}, E8{}) || pick(I1024{}, I1{}, E4{})) return;
+    using E16 = std::integral_constant<int, 16>;
+    if (pick(I2048{}, I1{}, E16{}) || pick(I2048{}, I1{}, E8{})) return;
+    if (pick(I1024{}, I2{}, E16{}) || pick(I1024{}, I2{}, E8{})) return;
+    if (pick(I1024{}, I1{}, E16{}) || pick(I1024{}, I1{}, E8{})) return;
     throw Error(FR_ERR_INVALID, "device: no kernel variant for (N, k, E)");
 }
 
@@ -519,19 +622,17 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
-    if ((e_ != 8 && e_ != 4) || (e_small_ != 8 && e_small_ != 4))
-        throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 4 or 8");
-    for (int e : {4, 8})
+    if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
+        throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
+    for (int e : {8, 16})
         dispatch(p_, e, [&](auto n, auto k, auto ec) { set_smem_attr<decltype(n)::value, decltype(k)::value, decltype(ec)::value>(); });
-    // twiddles
+    // Montgomery-form forward twiddles, per prime: zeta_q[k] * 2^32 mod p_q
     NttTables T(p.N);
-    std::vector<uint64_t> tw(2 * (size_t)p.N);
-    for (int i = 0; i < p.N; ++i) {
-        tw[i] = T.zeta[i];
-        tw[p.N + i] = T.izeta[i];
-    }
-    HIP_CHECK(hipMalloc(&d_tw_, 8 * tw.size()));
-    HIP_CHECK(hipMemcpy(d_tw_, tw.data(), 8 * tw.size(), hipMemcpyHostToDevice));
+    std::vector<uint32_t> tw(2 * (size_t)p.N);
+    for (int q = 0; q < 2; ++q)
+        for (int i = 0; i < p.N; ++i) tw[(size_t)q * p.N + i] = (uint32_t)(((uint64_t)T.zeta[q][i] << 32) % rns::prime(q));
+    HIP_CHECK(hipMalloc(&d_tw_, 4 * tw.size()));
+    HIP_CHECK(hipMemcpy(d_tw_, tw.data(), 4 * tw.size(), hipMemcpyHostToDevice));
     ensure_arena(1024);
     ensure_batch(1024);
 }
@@ -622,18 +723,31 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
     if (bsk.size() != (size_t)p_.n * kp1 * kp1 * p_.N) throw Error(FR_ERR_INVALID, "bsk size");
     (void)hipFree(d_ksk_);
     (void)hipFree(d_bsk_);
-    d_ksk_ = d_bsk_ = nullptr;
+    d_ksk_ = nullptr;
+    d_bsk_ = nullptr;
     HIP_CHECK(hipMalloc(&d_ksk_, 8 * ksk.size()));
     HIP_CHECK(hipMemcpy(d_ksk_, ksk.data(), 8 * ksk.size(), hipMemcpyHostToDevice));
     uint64_t* coef = nullptr;
     HIP_CHECK(hipMalloc(&coef, 8 * bsk.size()));
     HIP_CHECK(hipMemcpy(coef, bsk.data(), 8 * bsk.size(), hipMemcpyHostToDevice));
-    HIP_CHECK(hipMalloc(&d_bsk_, 8 * bsk.size()));
-    const uint64_t n_inv = gl_pow((uint64_t)p_.N, P - 2);
+    HIP_CHECK(hipMalloc(&d_bsk_, 4 * 2 * bsk.size()));  // two u32 residues per coefficient
+    // 1/N in Montgomery form per prime
+    uint32_t ninv_r[2];
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t pq = rns::prime(q);
+        uint64_t inv = 1, b = (uint64_t)p_.N % pq, e = pq - 2;
+        while (e) {
+            if (e & 1) inv = inv * b % pq;
+            b = b * b % pq;
+            e >>= 1;
+        }
+        ninv_r[q] = (uint32_t)((inv << 32) % pq);
+    }
     const int blocks = p_.n * (p_.k + 1);
     dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
         constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
-        k_bsk_to_ntt<N, K, E><<<blocks, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(coef, d_tw_, n_inv, d_bsk_);
+        k_bsk_to_ntt<N, K, E><<<blocks, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(coef, d_tw_, ninv_r[0],
+                                                                                                    ninv_r[1], d_bsk_);
     });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(STREAM));
@@ -804,13 +918,25 @@ void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, u
     HIP_CHECK(hipMalloc(&dout, 8 * count * N));
     HIP_CHECK(hipMemcpy(da, a, 8 * count * N, hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(db, b, 8 * count * N, hipMemcpyHostToDevice));
-    const uint64_t n_inv = gl_pow((uint64_t)N, P - 2);
+    // R^2 / N mod p (Montgomery: turns mont(a, b) = ab/R into ab/N)
+    uint32_t r2n[2];
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t pq = rns::prime(q);
+        uint64_t inv = 1, b = (uint64_t)N % pq, e = pq - 2;
+        while (e) {
+            if (e & 1) inv = inv * b % pq;
+            b = b * b % pq;
+            e >>= 1;
+        }
+        const uint64_t r2 = q ? rns::R2_1 : rns::R2_0;
+        r2n[q] = (uint32_t)(r2 * inv % pq);
+    }
     dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
         constexpr int NN = decltype(n_)::value, E = decltype(e_c)::value;
         (void)k_;
-        const size_t sm = 8 * (2 * (size_t)NttGeo<NN, E>::NP + (size_t)NN);
+        const size_t sm = 4 * (4 * (size_t)NttGeo<NN, E>::NP + 2 * (size_t)NN);
         HIP_CHECK(hipFuncSetAttribute((const void*)k_ring_mul<NN, E>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sm));
-        k_ring_mul<NN, E><<<(unsigned)count, 2 * (NN / E), sm, STREAM>>>(da, db, d_tw_, n_inv, dout);
+        k_ring_mul<NN, E><<<(unsigned)count, 4 * (NN / E), sm, STREAM>>>(da, db, d_tw_, r2n[0], r2n[1], dout);
     });
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipStreamSynchronize(STREAM));

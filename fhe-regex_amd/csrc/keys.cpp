@@ -2,9 +2,11 @@
 // encryption.  Follows tfhe-rs 0.2 shortint semantics as used by the reference
 // (src/regex/ciphertext.rs:32-45, src/regex/engine.rs:248-254): LWE encryption
 // under the big (flattened GLWE) key with glwe noise, KSK big->small under the
-// LWE noise, GGSW bootstrapping key with one 2^23 gadget level.  The GGSW ring
-// is Z_p[X]/(X^N+1), p = 2^64-2^32+1.
+// LWE noise, GGSW bootstrapping key with one gadget level (g = round(Q/2^23)).
+// The GGSW ring is Z_Q[X]/(X^N+1), Q = p0*p1 in RNS form (rns.h).
 #include "keys.h"
+
+#include "rns.h"
 
 #include <cmath>
 #include <cstring>
@@ -48,18 +50,32 @@ uint64_t Rng::u64(uint64_t idx) {
     return (uint64_t)w_[o] | ((uint64_t)w_[o + 1] << 32);
 }
 
-int64_t Rng::gaussian(uint64_t idx, double sigma) {
+int64_t Rng::gaussian(uint64_t idx, double sigma, double scale) {
     uint64_t x1 = u64(2 * idx), x2 = u64(2 * idx + 1);
     double u1 = (double)((x1 >> 11) + 1) * 0x1.0p-53;
     double u2 = (double)(x2 >> 11) * 0x1.0p-53;
     double rad = std::sqrt(-2.0 * std::log(u1));
     double z = rad * std::cos(6.283185307179586 * u2);
-    double scaled = z * (sigma * 18446744073709551616.0);
+    double scaled = z * (sigma * scale);
     return (int64_t)std::llround(scaled);
 }
 
-static inline uint64_t zp_from_i64(int64_t v) {
-    return v >= 0 ? (uint64_t)v % P : P - ((uint64_t)(-v) % P);
+using rns::Q;
+static inline uint64_t q_add(uint64_t a, uint64_t b) { uint64_t s = a + b; return s >= Q ? s - Q : s; }
+static inline uint64_t zq_from_i64(int64_t v) {
+    if (v >= 0) return (uint64_t)v % Q;
+    uint64_t m = (uint64_t)(-v) % Q;
+    return m ? Q - m : 0;
+}
+static inline uint64_t pow_mod(uint64_t b, uint64_t e, uint64_t p) {
+    uint64_t r = 1;
+    b %= p;
+    while (e) {
+        if (e & 1) r = r * b % p;
+        b = b * b % p;
+        e >>= 1;
+    }
+    return r;
 }
 
 // ---------------------------------------------------------------- key parse
@@ -124,44 +140,67 @@ static int brv(int x, int bits) {
 NttTables::NttTables(int N_) : N(N_) {
     logN = 0;
     while ((1 << logN) < N) ++logN;
-    uint64_t psi = gl_pow(7, (P - 1) / (2 * (uint64_t)N));
-    uint64_t ipsi = gl_pow(psi, 2 * (uint64_t)N - 1);
-    zeta.resize(N);
-    izeta.resize(N);
-    for (int k = 0; k < N; ++k) {
-        zeta[k] = gl_pow(psi, (uint64_t)brv(k, logN));
-        izeta[k] = gl_pow(ipsi, (uint64_t)brv(k, logN));
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t p = rns::prime(q);
+        const uint64_t psi = pow_mod(rns::GENERATOR, (p - 1) / (2 * (uint64_t)N), p);
+        const uint64_t ipsi = pow_mod(psi, p - 2, p);
+        zeta[q].resize(N);
+        izeta[q].resize(N);
+        for (int k = 0; k < N; ++k) {
+            zeta[q][k] = (uint32_t)pow_mod(psi, (uint64_t)brv(k, logN), p);
+            izeta[q][k] = (uint32_t)pow_mod(ipsi, (uint64_t)brv(k, logN), p);
+        }
+        n_inv[q] = (uint32_t)pow_mod((uint64_t)N, p - 2, p);
     }
-    n_inv = gl_pow((uint64_t)N, P - 2);
 }
 
-void NttTables::forward(uint64_t* a) const {
+void NttTables::forward(int q, uint32_t* a) const {
+    const uint64_t p = rns::prime(q);
     for (int s = 0; s < logN; ++s) {
         int L = N >> (s + 1);
         for (int start = 0; start < N; start += 2 * L) {
-            uint64_t z = zeta[(1 << s) + start / (2 * L)];
+            uint64_t z = zeta[q][(1 << s) + start / (2 * L)];
             for (int j = start; j < start + L; ++j) {
-                uint64_t t = gl_mul(z, a[j + L]);
-                a[j + L] = gl_sub(a[j], t);
-                a[j] = gl_add(a[j], t);
+                uint64_t t = z * a[j + L] % p;
+                a[j + L] = (uint32_t)((a[j] + p - t) % p);
+                a[j] = (uint32_t)((a[j] + t) % p);
             }
         }
     }
 }
 
-void NttTables::inverse(uint64_t* a) const {
+void NttTables::inverse(int q, uint32_t* a) const {
+    const uint64_t p = rns::prime(q);
     for (int s = logN - 1; s >= 0; --s) {
         int L = N >> (s + 1);
         for (int start = 0; start < N; start += 2 * L) {
-            uint64_t z = izeta[(1 << s) + start / (2 * L)];
+            uint64_t z = izeta[q][(1 << s) + start / (2 * L)];
             for (int j = start; j < start + L; ++j) {
                 uint64_t u = a[j], v = a[j + L];
-                a[j] = gl_add(u, v);
-                a[j + L] = gl_mul(gl_sub(u, v), z);
+                a[j] = (uint32_t)((u + v) % p);
+                a[j + L] = (uint32_t)((u + p - v) % p * z % p);
             }
         }
     }
-    for (int j = 0; j < N; ++j) a[j] = gl_mul(a[j], n_inv);
+    for (int j = 0; j < N; ++j) a[j] = (uint32_t)((uint64_t)a[j] * n_inv[q] % p);
+}
+
+void ring_mul_q(const NttTables& T, const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    const int N = T.N;
+    std::vector<uint32_t> x[2], y(N);
+    for (int q = 0; q < 2; ++q) {
+        const uint64_t p = rns::prime(q);
+        x[q].resize(N);
+        for (int t = 0; t < N; ++t) {
+            x[q][t] = (uint32_t)(a[t] % p);
+            y[t] = (uint32_t)(b[t] % p);
+        }
+        T.forward(q, x[q].data());
+        T.forward(q, y.data());
+        for (int t = 0; t < N; ++t) x[q][t] = (uint32_t)((uint64_t)x[q][t] * y[t] % p);
+        T.inverse(q, x[q].data());
+    }
+    for (int t = 0; t < N; ++t) out[t] = rns::crt(x[0][t], x[1][t]);
 }
 
 // ---------------------------------------------------------------- keygen
@@ -203,33 +242,42 @@ void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
     const size_t kp1 = (size_t)k + 1;
     bsk.assign((size_t)n * kp1 * kp1 * N, 0);
     NttTables T(N);
-    std::vector<uint64_t> S((size_t)k * N);
-    for (int j = 0; j < k; ++j) {
-        for (int t = 0; t < N; ++t) S[(size_t)j * N + t] = ck.s_big[(size_t)j * N + t];
-        T.forward(S.data() + (size_t)j * N);
+    // NTT of the key polynomials S_j, per prime
+    std::vector<uint32_t> S[2];
+    for (int q = 0; q < 2; ++q) {
+        S[q].resize((size_t)k * N);
+        for (int j = 0; j < k; ++j) {
+            for (int t = 0; t < N; ++t) S[q][(size_t)j * N + t] = (uint32_t)ck.s_big[(size_t)j * N + t];
+            T.forward(q, S[q].data() + (size_t)j * N);
+        }
     }
     parallel_for(n, [&](int i) {
         Rng rm(seed, STREAM_BSK_MASK), rn(seed, STREAM_BSK_NOISE);
-        std::vector<uint64_t> tmp(N), acc(N);
+        std::vector<uint32_t> tmp(N), acc[2] = {std::vector<uint32_t>(N), std::vector<uint32_t>(N)};
         for (size_t r = 0; r < kp1; ++r) {
             uint64_t* row = bsk.data() + ((size_t)i * kp1 + r) * kp1 * N;
-            std::fill(acc.begin(), acc.end(), 0);
+            std::fill(acc[0].begin(), acc[0].end(), 0);
+            std::fill(acc[1].begin(), acc[1].end(), 0);
             for (int j = 0; j < k; ++j) {
                 uint64_t* A = row + (size_t)j * N;
                 uint64_t base = (((uint64_t)i * kp1 + r) * k + j) * N;
-                for (int t = 0; t < N; ++t) {
-                    uint64_t x = rm.u64(base + t);
-                    A[t] = x >= P ? x - P : x;
+                // uniform mask in [0, Q): floor(x * Q / 2^64)
+                for (int t = 0; t < N; ++t) A[t] = (uint64_t)(((unsigned __int128)rm.u64(base + t) * Q) >> 64);
+                for (int q = 0; q < 2; ++q) {
+                    const uint64_t pq = rns::prime(q);
+                    for (int t = 0; t < N; ++t) tmp[t] = (uint32_t)(A[t] % pq);
+                    T.forward(q, tmp.data());
+                    const uint32_t* Sj = S[q].data() + (size_t)j * N;
+                    for (int t = 0; t < N; ++t) acc[q][t] = (uint32_t)((acc[q][t] + (uint64_t)tmp[t] * Sj[t]) % pq);
                 }
-                std::memcpy(tmp.data(), A, 8 * (size_t)N);
-                T.forward(tmp.data());
-                for (int t = 0; t < N; ++t) acc[t] = gl_add(acc[t], gl_mul(tmp[t], S[(size_t)j * N + t]));
             }
-            T.inverse(acc.data());
+            T.inverse(0, acc[0].data());
+            T.inverse(1, acc[1].data());
             uint64_t* Bp = row + (size_t)k * N;
             uint64_t nb = ((uint64_t)i * kp1 + r) * N;
-            for (int t = 0; t < N; ++t) Bp[t] = gl_add(acc[t], zp_from_i64(rn.gaussian(nb + t, p.glwe_sigma)));
-            if (ck.s_small[i]) row[r * N] = gl_add(row[r * N], PBS_G);
+            for (int t = 0; t < N; ++t)
+                Bp[t] = q_add(rns::crt(acc[0][t], acc[1][t]), zq_from_i64(rn.gaussian(nb + t, p.glwe_sigma, (double)Q)));
+            if (ck.s_small[i]) row[r * N] = q_add(row[r * N], rns::G);
         }
     });
 }

@@ -25,8 +25,9 @@ class Rng {
   public:
     Rng(uint64_t seed, uint64_t stream) : seed_(seed), stream_(stream) {}
     uint64_t u64(uint64_t idx);
-    // Box-Muller on words 2*idx, 2*idx+1; rounded to 2^-64 torus units.
-    int64_t gaussian(uint64_t idx, double sigma);
+    // Box-Muller on words 2*idx, 2*idx+1; z * sigma * scale rounded to an
+    // integer (scale 2^64: torus units; scale Q: units of Z_Q).
+    int64_t gaussian(uint64_t idx, double sigma, double scale = 18446744073709551616.0);
 
   private:
     uint64_t seed_, stream_, blk_ = 0;
@@ -48,7 +49,7 @@ ClientKey parse_client_key(const uint8_t* data, size_t len);
 
 // KSK: [i in kN][level j][t in n+1], torus 2^64.
 void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& ksk);
-// BSK: [i in n][row r in k+1][component c in k+1][coef], coefficient domain mod P.
+// BSK: [i in n][row r in k+1][component c in k+1][coef], coefficient domain mod Q (rns.h).
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk);
 
 // Fresh LWE encryptions of block messages (Delta = 2^59) under the big key.
@@ -58,15 +59,18 @@ uint64_t lwe_phase(const Params& p, const ClientKey& ck, const uint64_t* lwe);
 // tfhe-rs shortint decrypt_message_and_carry: round(phase / Delta) mod 16
 uint32_t decode16(uint64_t phase);
 
-// Host negacyclic NTT over Z_p (merged-psi Cooley-Tukey / Gentleman-Sande,
-// bit-reversed evaluation order) — used by keygen and for device twiddles.
+// Host negacyclic NTT over Z_p for the two RNS primes (merged-psi
+// Cooley-Tukey / Gentleman-Sande, bit-reversed evaluation order) — used by
+// keygen and for the device twiddles.  Canonical residues, plain '%' math.
 struct NttTables {
     int N = 0, logN = 0;
-    std::vector<uint64_t> zeta, izeta;  // zeta[k] = psi^brv(k), izeta[k] = psi^-brv(k)
-    uint64_t n_inv = 0;
+    std::vector<uint32_t> zeta[2], izeta[2];  // zeta[k] = psi^brv(k), izeta[k] = psi^-brv(k)
+    uint32_t n_inv[2] = {0, 0};
     explicit NttTables(int N);
-    void forward(uint64_t* a) const;
-    void inverse(uint64_t* a) const;  // includes the 1/N factor
+    void forward(int q, uint32_t* a) const;
+    void inverse(int q, uint32_t* a) const;  // includes the 1/N factor
 };
+// negacyclic product mod Q of a, b in [0, Q)
+void ring_mul_q(const NttTables& T, const uint64_t* a, const uint64_t* b, uint64_t* out);
 
 }  // namespace fr

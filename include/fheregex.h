@@ -199,7 +199,8 @@ int fr_dev_blind_rotate(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, si
  * rotated itself; else multi-value) -> out: n_out*(kN+1) */
 int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* luts, int32_t n_out, int32_t direct,
                               uint64_t* out);
-/* negacyclic product in Z_p[X]/(X^N+1) through the device NTT: count pairs */
+/* negacyclic product in Z_Q[X]/(X^N+1) (Q = 998244353 * 1004535809, inputs in
+ * [0, Q)) through the device RNS NTT: count pairs */
 int fr_dev_ring_mul(fr_ctx* ctx, const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out);
 /* Full timed PBS batch for roofline measurement: count gates of the given
  * lut over the uploaded boolean/radix handles; returns BR kernel ms. */
@@ -207,8 +208,9 @@ int fr_dev_bench_pbs(fr_ctx* ctx, const fr_ct* in, size_t count, int32_t iters, 
 
 int fr_device_info(fr_ctx* ctx, char* buf, size_t buflen);
 
-/* Scalar maps shared by host and device code (test hook): op 0 = Z_p product
- * x*y, 1 = PBS gadget digit of x (Z_p), 2 = Z_p -> 2^64 torus of x,
+/* Scalar maps shared by host and device code (test hook): op 0 = CRT of the
+ * residues of x (identity on [0, Q)), 1 = PBS gadget digit of x mod Q (signed,
+ * as u64), 2 = Z_Q -> 2^64 torus of x mod Q (from its residues),
  * 3 = modulus switch of x to 2^y, 4 = keyswitch digit y (0..4) of x (signed, as u64). */
 uint64_t fr_debug_scalar(int32_t op, uint64_t x, uint64_t y);
 

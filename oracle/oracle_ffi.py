@@ -16,7 +16,8 @@ import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
-P_GOLDILOCKS = 0xFFFFFFFF00000001
+Q_RING = 998244353 * 1004535809  # GLWE/GGSW ring modulus (RNS: two NTT primes)
+RNS_PRIMES = (998244353, 1004535809)
 
 
 class Params(C.Structure):
@@ -55,8 +56,10 @@ def lib():
             build()
         L = C.CDLL(LIB_PATH)
         u64p = C.POINTER(C.c_uint64)
-        L.or_gl_mul.restype = C.c_uint64
-        L.or_gl_mul.argtypes = [C.c_uint64, C.c_uint64]
+        L.or_q_mul.restype = C.c_uint64
+        L.or_q_mul.argtypes = [C.c_uint64, C.c_uint64]
+        L.or_q_modulus.restype = C.c_uint64
+        L.or_pbs_gadget.restype = C.c_uint64
         L.or_rng_u64.restype = C.c_uint64
         L.or_rng_u64.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
         L.or_gaussian.restype = C.c_int64

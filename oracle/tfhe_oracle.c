@@ -13,11 +13,13 @@
  * the reference fixture test_data/client_key (PARAM_MESSAGE_2_CARRY_2:
  * n=742, k=1, N=2048, PBS 2^23 x 1, KS 2^3 x 5, Delta = 2^59), with one
  * documented deviation shared with the GPU product: the GLWE/GGSW ring is
- * Z_p[X]/(X^N+1) with p = 2^64 - 2^32 + 1 (exact integer NTT) instead of
- * tfhe-rs's torus 2^64 with an f64 FFT; sample-extracted LWEs are mapped back
- * to the 2^64 torus by x -> round(x * 2^64 / p) so every ciphertext that
- * crosses the boundary decrypts with the reference's client key and the
- * tfhe-rs decoding rule (shortint decrypt_message_and_carry).
+ * Z_Q[X]/(X^N+1) with Q = 998244353 * 1004535809 (~2^59.8, exact integer
+ * NTTs per prime + CRT) instead of tfhe-rs's torus 2^64 with an f64 FFT;
+ * sample-extracted LWEs are mapped back to the 2^64 torus by
+ * x -> sum_i round(2^64 * u_i / p_i) (u_i = x * (Q/p_i)^-1 mod p_i, which is
+ * round(x * 2^64 / Q) up to one unit) so every ciphertext that crosses the
+ * boundary decrypts with the reference's client key and the tfhe-rs decoding
+ * rule (shortint decrypt_message_and_carry).
  *
  * Call sites in the reference this path replaces: src/regex/execution.rs:76,
  * 93,110,143,173,190 (smart_eq/gt/le/bitand/bitor/bitxor), trivial constants
@@ -27,8 +29,11 @@
  * Parity pins: the fixture client key (decoding verified in tests), the 25
  * decrypted-result cases of src/regex/engine.rs:256-280, and bit-identity with
  * the GPU path (same keys, same inputs).  The ring product here is a textbook
- * twisted cyclic NTT, written independently of the GPU's merged-psi NTT; both
- * are exact in Z_p so the products agree bit for bit.
+ * twisted cyclic NTT per prime with 64-bit '%' arithmetic and a 128-bit CRT,
+ * written independently of the GPU's lazy Montgomery merged-psi NTT; both are
+ * exact in Z_Q so the products agree bit for bit.  Likewise the boundary maps
+ * (gadget digit, Z_Q -> torus) use plain 128-bit division here and
+ * reciprocal/Montgomery forms on the GPU.
  */
 #include <math.h>
 #include <stdint.h>
@@ -37,7 +42,9 @@
 
 typedef unsigned __int128 u128;
 
-#define GL_P 0xFFFFFFFF00000001ULL
+/* RNS ring: Q = p0 * p1 */
+static const uint64_t PR[2] = {998244353ULL, 1004535809ULL};
+#define Q_MOD (998244353ULL * 1004535809ULL)
 
 /* ---------------------------------------------------------------- params */
 typedef struct {
@@ -53,33 +60,28 @@ typedef struct {
     double glwe_sigma;    /* BSK / fresh-encryption noise */
 } or_params;
 
-/* ----------------------------------------------------------- Goldilocks */
-static inline uint64_t gl_reduce128(u128 x) {
-    /* x = lo + hl*2^64 + hh*2^96 ; 2^64 = 2^32-1, 2^96 = -1 (mod p) */
-    uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
-    uint64_t hh = hi >> 32, hl = hi & 0xFFFFFFFFULL;
-    uint64_t t = lo - hh;
-    if (lo < hh) t -= 0xFFFFFFFFULL;            /* borrow: + p */
-    uint64_t u = hl * 0xFFFFFFFFULL;
-    uint64_t r = t + u;
-    if (r < t) r += 0xFFFFFFFFULL;              /* carry: + 2^64 = 2^32-1 */
-    return r >= GL_P ? r - GL_P : r;
-}
-static inline uint64_t gl_add(uint64_t a, uint64_t b) {
-    uint64_t s = a + b;
-    if (s < a) s += 0xFFFFFFFFULL;
-    return s >= GL_P ? s - GL_P : s;
-}
-static inline uint64_t gl_sub(uint64_t a, uint64_t b) { return a >= b ? a - b : a + (GL_P - b); }
-static inline uint64_t gl_mul(uint64_t a, uint64_t b) { return gl_reduce128((u128)a * b); }
-static uint64_t gl_pow(uint64_t b, uint64_t e) {
+/* ------------------------------------------------------------ Z_Q, Z_p */
+static inline uint64_t q_add(uint64_t a, uint64_t b) { uint64_t s = a + b; return s >= Q_MOD ? s - Q_MOD : s; }
+static inline uint64_t q_sub(uint64_t a, uint64_t b) { return a >= b ? a - b : a + (Q_MOD - b); }
+static inline uint64_t q_neg(uint64_t a) { return a ? Q_MOD - a : 0; }
+static inline uint64_t q_mul(uint64_t a, uint64_t b) { return (uint64_t)(((u128)a * b) % Q_MOD); }
+static inline uint64_t q_from_i64(int64_t v) { return v >= 0 ? (uint64_t)v % Q_MOD : q_neg((uint64_t)(-v) % Q_MOD); }
+static uint64_t pm_pow(uint64_t b, uint64_t e, uint64_t p) {
     uint64_t r = 1;
-    while (e) { if (e & 1) r = gl_mul(r, b); b = gl_mul(b, b); e >>= 1; }
+    b %= p;
+    while (e) { if (e & 1) r = r * b % p; b = b * b % p; e >>= 1; }
     return r;
 }
-static inline uint64_t gl_from_i64(int64_t v) { return v >= 0 ? (uint64_t)v % GL_P : GL_P - ((uint64_t)(-v) % GL_P); }
+/* CRT of residues r0 mod p0, r1 mod p1 -> [0, Q) */
+static inline uint64_t crt2(uint64_t r0, uint64_t r1) {
+    static uint64_t inv = 0;
+    if (!inv) inv = pm_pow(PR[0], PR[1] - 2, PR[1]);
+    uint64_t k = (r1 + PR[1] - r0 % PR[1]) % PR[1] * inv % PR[1];
+    return r0 + PR[0] * k;
+}
 
-uint64_t or_gl_mul(uint64_t a, uint64_t b) { return gl_mul(a, b); }
+uint64_t or_q_mul(uint64_t a, uint64_t b) { return q_mul(a, b); }
+uint64_t or_q_modulus(void) { return Q_MOD; }
 
 /* ------------------------------------------------------------- ChaCha20 */
 #define ROTL32(a, b) (((a) << (b)) | ((a) >> (32 - (b))))
@@ -116,26 +118,29 @@ static inline rng_t rng_make(uint64_t seed, uint64_t stream) { rng_t r; r.seed =
 enum { STREAM_KSK_MASK = 1, STREAM_KSK_NOISE = 2, STREAM_BSK_MASK = 3, STREAM_BSK_NOISE = 4,
        STREAM_ENC_MASK = 5, STREAM_ENC_NOISE = 6 };
 
-/* Box-Muller on two stream words; rounded to an integer number of 2^-64 torus units */
-static int64_t gaussian(rng_t* r, uint64_t idx, double sigma) {
+/* Box-Muller on two stream words; z * sigma * scale rounded to an integer
+ * (scale 2^64: torus units; scale Q: units of Z_Q) */
+#define TORUS_SCALE 18446744073709551616.0
+static int64_t gaussian_s(rng_t* r, uint64_t idx, double sigma, double scale) {
     uint64_t x1 = rng_u64(r, 2 * idx), x2 = rng_u64(r, 2 * idx + 1);
     double u1 = (double)((x1 >> 11) + 1) * 0x1.0p-53;
     double u2 = (double)(x2 >> 11) * 0x1.0p-53;
     double rad = sqrt(-2.0 * log(u1));
     double z = rad * cos(6.283185307179586 * u2);
-    double scaled = z * (sigma * 18446744073709551616.0);
+    double scaled = z * (sigma * scale);
     return (int64_t)llround(scaled);
 }
+static int64_t gaussian(rng_t* r, uint64_t idx, double sigma) { return gaussian_s(r, idx, sigma, TORUS_SCALE); }
 
 uint64_t or_rng_u64(uint64_t seed, uint64_t stream, uint64_t idx) { rng_t r = rng_make(seed, stream); return rng_u64(&r, idx); }
 int64_t or_gaussian(uint64_t seed, uint64_t stream, uint64_t idx, double sigma) { rng_t r = rng_make(seed, stream); return gaussian(&r, idx, sigma); }
 
-/* ------------------------------------------------- textbook negacyclic NTT */
+/* ------------------------------------------- textbook negacyclic NTT mod p */
 typedef struct {
     int N, logN;
-    uint64_t *psi, *psi_inv;  /* psi^i, psi^-i (i < N) */
-    uint64_t *w, *w_inv;      /* omega^i (i < N/2), omega = psi^2 */
-    uint64_t n_inv;
+    uint64_t *psi[2], *psi_inv[2];  /* psi^i, psi^-i (i < N) per prime */
+    uint64_t *w[2], *w_inv[2];      /* omega^i, omega = psi^2 */
+    uint64_t n_inv[2];
 } ntt_plan;
 
 static int ilog2(int x) { int l = 0; while ((1 << l) < x) l++; return l; }
@@ -143,21 +148,27 @@ static int ilog2(int x) { int l = 0; while ((1 << l) < x) l++; return l; }
 static ntt_plan* ntt_plan_make(int N) {
     ntt_plan* P = (ntt_plan*)calloc(1, sizeof(ntt_plan));
     P->N = N; P->logN = ilog2(N);
-    uint64_t psi = gl_pow(7, (GL_P - 1) / (2 * (uint64_t)N));
-    uint64_t psi_inv = gl_pow(psi, 2 * (uint64_t)N - 1);
-    P->psi = malloc(8 * N); P->psi_inv = malloc(8 * N); P->w = malloc(8 * N); P->w_inv = malloc(8 * N);
-    uint64_t a = 1, b = 1;
-    for (int i = 0; i < N; i++) { P->psi[i] = a; P->psi_inv[i] = b; a = gl_mul(a, psi); b = gl_mul(b, psi_inv); }
-    uint64_t om = gl_mul(psi, psi), omi = gl_mul(psi_inv, psi_inv);
-    a = 1; b = 1;
-    for (int i = 0; i < N; i++) { P->w[i] = a; P->w_inv[i] = b; a = gl_mul(a, om); b = gl_mul(b, omi); }
-    P->n_inv = gl_pow((uint64_t)N, GL_P - 2);
+    for (int q = 0; q < 2; q++) {
+        uint64_t p = PR[q];
+        uint64_t psi = pm_pow(3, (p - 1) / (2 * (uint64_t)N), p); /* 3 generates Z_p^* */
+        uint64_t psi_inv = pm_pow(psi, p - 2, p);
+        P->psi[q] = malloc(8 * N); P->psi_inv[q] = malloc(8 * N); P->w[q] = malloc(8 * N); P->w_inv[q] = malloc(8 * N);
+        uint64_t a = 1, b = 1;
+        for (int i = 0; i < N; i++) { P->psi[q][i] = a; P->psi_inv[q][i] = b; a = a * psi % p; b = b * psi_inv % p; }
+        uint64_t om = psi * psi % p, omi = psi_inv * psi_inv % p;
+        a = 1; b = 1;
+        for (int i = 0; i < N; i++) { P->w[q][i] = a; P->w_inv[q][i] = b; a = a * om % p; b = b * omi % p; }
+        P->n_inv[q] = pm_pow((uint64_t)N, p - 2, p);
+    }
     return P;
 }
-static void ntt_plan_free(ntt_plan* P) { free(P->psi); free(P->psi_inv); free(P->w); free(P->w_inv); free(P); }
+static void ntt_plan_free(ntt_plan* P) {
+    for (int q = 0; q < 2; q++) { free(P->psi[q]); free(P->psi_inv[q]); free(P->w[q]); free(P->w_inv[q]); }
+    free(P);
+}
 
-/* cyclic DIT NTT (bit-reverse, then butterflies) over w[] (forward) or w_inv[] */
-static void cyclic_ntt(const ntt_plan* P, uint64_t* a, const uint64_t* w) {
+/* cyclic DIT NTT mod p (bit-reverse, then butterflies) over w[] or w_inv[] */
+static void cyclic_ntt(const ntt_plan* P, uint64_t p, uint64_t* a, const uint64_t* w) {
     int N = P->N, L = P->logN;
     for (int i = 0; i < N; i++) {
         int r = 0;
@@ -168,58 +179,80 @@ static void cyclic_ntt(const ntt_plan* P, uint64_t* a, const uint64_t* w) {
         int step = N / len;
         for (int s = 0; s < N; s += len)
             for (int j = 0; j < len / 2; j++) {
-                uint64_t u = a[s + j], v = gl_mul(a[s + j + len / 2], w[j * step]);
-                a[s + j] = gl_add(u, v);
-                a[s + j + len / 2] = gl_sub(u, v);
+                uint64_t u = a[s + j], v = a[s + j + len / 2] * w[j * step] % p;
+                a[s + j] = (u + v) % p;
+                a[s + j + len / 2] = (u + p - v) % p;
             }
     }
 }
-/* forward negacyclic transform: twist by psi^i then cyclic NTT */
-static void nega_forward(const ntt_plan* P, uint64_t* a) {
-    for (int i = 0; i < P->N; i++) a[i] = gl_mul(a[i], P->psi[i]);
-    cyclic_ntt(P, a, P->w);
+/* forward negacyclic transform mod PR[q]: twist by psi^i then cyclic NTT */
+static void nega_forward(const ntt_plan* P, int q, uint64_t* a) {
+    uint64_t p = PR[q];
+    for (int i = 0; i < P->N; i++) a[i] = a[i] % p * P->psi[q][i] % p;
+    cyclic_ntt(P, p, a, P->w[q]);
 }
-static void nega_inverse(const ntt_plan* P, uint64_t* a) {
-    cyclic_ntt(P, a, P->w_inv);
-    for (int i = 0; i < P->N; i++) a[i] = gl_mul(gl_mul(a[i], P->n_inv), P->psi_inv[i]);
+static void nega_inverse(const ntt_plan* P, int q, uint64_t* a) {
+    uint64_t p = PR[q];
+    cyclic_ntt(P, p, a, P->w_inv[q]);
+    for (int i = 0; i < P->N; i++) a[i] = a[i] * P->n_inv[q] % p * P->psi_inv[q][i] % p;
 }
 
+/* negacyclic product mod Q of a, b in [0, Q) */
+static void ring_mul_q(const ntt_plan* P, const uint64_t* a, const uint64_t* b, uint64_t* out) {
+    int N = P->N;
+    uint64_t* x[2]; uint64_t* y = malloc(8 * N);
+    for (int q = 0; q < 2; q++) {
+        x[q] = malloc(8 * N);
+        for (int i = 0; i < N; i++) { x[q][i] = a[i] % PR[q]; y[i] = b[i] % PR[q]; }
+        nega_forward(P, q, x[q]); nega_forward(P, q, y);
+        for (int i = 0; i < N; i++) x[q][i] = x[q][i] * y[i] % PR[q];
+        nega_inverse(P, q, x[q]);
+    }
+    for (int i = 0; i < N; i++) out[i] = crt2(x[0][i], x[1][i]);
+    free(x[0]); free(x[1]); free(y);
+}
 void or_ring_mul(int N, const uint64_t* a, const uint64_t* b, uint64_t* out) {
     ntt_plan* P = ntt_plan_make(N);
-    uint64_t* x = malloc(8 * N); uint64_t* y = malloc(8 * N);
-    memcpy(x, a, 8 * N); memcpy(y, b, 8 * N);
-    nega_forward(P, x); nega_forward(P, y);
-    for (int i = 0; i < N; i++) x[i] = gl_mul(x[i], y[i]);
-    nega_inverse(P, x);
-    memcpy(out, x, 8 * N);
-    free(x); free(y); ntt_plan_free(P);
+    ring_mul_q(P, a, b, out);
+    ntt_plan_free(P);
 }
 void or_ring_mul_schoolbook(int N, const uint64_t* a, const uint64_t* b, uint64_t* out) {
     for (int i = 0; i < N; i++) out[i] = 0;
     for (int i = 0; i < N; i++)
         for (int j = 0; j < N; j++) {
-            uint64_t m = gl_mul(a[i], b[j]);
+            uint64_t m = q_mul(a[i], b[j]);
             int d = i + j;
-            if (d < N) out[d] = gl_add(out[d], m);
-            else out[d - N] = gl_sub(out[d - N], m);
+            if (d < N) out[d] = q_add(out[d], m);
+            else out[d - N] = q_sub(out[d - N], m);
         }
 }
 
 /* ------------------------------------------------ decompositions & maps */
-/* PBS gadget (base 2^23, 1 level) in Z_p: g = floor(p / 2^23) = 2^41 - 2^9,
- * 2^23 * g = p - 1 = -1.  digit = round(x / g) in [0, 2^23], recentred to
- * [-2^22, 2^22); the wrap costs an error of exactly 1.  Returned in Z_p. */
-uint64_t or_decompose_pbs(uint64_t x) {
-    const uint64_t g = (1ULL << 41) - (1ULL << 9);
-    uint64_t d = (uint64_t)(((u128)x + g / 2) / g);
-    if (d >= (1ULL << 22)) return GL_P - ((1ULL << 23) - d); /* d - 2^23 < 0 */
-    return d;
+/* PBS gadget (base 2^23, 1 level) in Z_Q: g = round(Q / 2^23).  Digit of x:
+ * write x = r0 + p0 * k (r0 = x mod p0, k = (x - r0) / p0 < p1), take
+ * t = (k * M + 2^37) >> 38 with M = round(2^61 / p1) (t ~ x * 2^23 / Q in
+ * [0, 2^23]) and recentre to [-2^22, 2^22).  Returned as int64. */
+static uint64_t pbs_g(void) { return (Q_MOD + (1ULL << 22)) >> 23; }
+static int64_t decompose_q(uint64_t x) {
+    const uint64_t p1 = PR[1];
+    const uint64_t M = ((1ULL << 61) + p1 / 2) / p1;
+    const uint64_t k = (x - x % PR[0]) / PR[0];
+    const uint64_t t = (uint64_t)(((u128)k * M + ((u128)1 << 37)) >> 38);
+    return t >= (1ULL << 22) ? (int64_t)t - (1LL << 23) : (int64_t)t;
 }
+uint64_t or_decompose_pbs(uint64_t x) { return (uint64_t)decompose_q(x); }
+uint64_t or_pbs_gadget(void) { return pbs_g(); }
 
-/* Z_p -> torus 2^64: round(x * 2^64 / p) */
+/* Z_Q -> torus 2^64 from the residues: sum_i round(2^64 * u_i / p_i) mod 2^64,
+ * u_i = x * (Q/p_i)^-1 mod p_i (CRT: sum_i u_i/p_i = x/Q mod 1). */
 uint64_t or_conv(uint64_t x) {
-    u128 num = ((u128)x << 64) + (GL_P - 1) / 2;
-    return (uint64_t)(num / GL_P);
+    uint64_t y = 0;
+    for (int q = 0; q < 2; q++) {
+        uint64_t p = PR[q], other = PR[1 - q];
+        uint64_t u = x % p * pm_pow(other, p - 2, p) % p;
+        y += (uint64_t)((((u128)u << 64) + (p - 1) / 2) / p);
+    }
+    return y;
 }
 
 /* signed base-2^B, L-level decomposition of the top B*L bits (rounded) */
@@ -259,19 +292,15 @@ void or_keygen_ksk(const or_params* P, const uint64_t* s_big, const uint64_t* s_
         }
 }
 
-/* BSK in the coefficient domain mod p; layout [i][r][c][t], r,c in [0,k] */
+/* BSK in the coefficient domain mod Q; layout [i][r][c][t], r,c in [0,k].
+ * GGSW row r of s_small[i]: a GLWE encryption of zero (mask uniform in Z_Q,
+ * body = sum_j A_j S_j + e) plus g * s_small[i] on component r. */
 void or_keygen_bsk(const or_params* P, const uint64_t* s_big, const uint64_t* s_small, uint64_t seed, uint64_t* bsk) {
     int k = P->k, N = P->N, n = P->n;
-    const uint64_t g = (1ULL << 41) - (1ULL << 9);
+    const uint64_t g = pbs_g();
     ntt_plan* NP = ntt_plan_make(N);
-    /* NTT of the key polynomials S_j (coefficients of the flattened big key) */
-    uint64_t* S = malloc(8 * (size_t)k * N);
-    for (int j = 0; j < k; j++) {
-        for (int t = 0; t < N; t++) S[(size_t)j * N + t] = s_big[(size_t)j * N + t];
-        nega_forward(NP, S + (size_t)j * N);
-    }
     rng_t rm = rng_make(seed, STREAM_BSK_MASK), rn = rng_make(seed, STREAM_BSK_NOISE);
-    uint64_t* tmp = malloc(8 * (size_t)N);
+    uint64_t* prod = malloc(8 * (size_t)N);
     uint64_t* acc = malloc(8 * (size_t)N);
     for (int i = 0; i < n; i++)
         for (int r = 0; r <= k; r++) {
@@ -280,19 +309,17 @@ void or_keygen_bsk(const or_params* P, const uint64_t* s_big, const uint64_t* s_
             for (int j = 0; j < k; j++) {
                 uint64_t* A = row + (size_t)j * N;
                 uint64_t base = (((uint64_t)i * (k + 1) + r) * k + j) * N;
-                for (int t = 0; t < N; t++) { uint64_t x = rng_u64(&rm, base + t); A[t] = x >= GL_P ? x - GL_P : x; }
-                memcpy(tmp, A, 8 * (size_t)N);
-                nega_forward(NP, tmp);
-                for (int t = 0; t < N; t++) acc[t] = gl_add(acc[t], gl_mul(tmp[t], S[(size_t)j * N + t]));
+                for (int t = 0; t < N; t++) A[t] = (uint64_t)(((u128)rng_u64(&rm, base + t) * Q_MOD) >> 64);
+                ring_mul_q(NP, A, s_big + (size_t)j * N, prod);
+                for (int t = 0; t < N; t++) acc[t] = q_add(acc[t], prod[t]);
             }
-            nega_inverse(NP, acc);
             uint64_t* Bp = row + (size_t)k * N;
             uint64_t nb = ((uint64_t)i * (k + 1) + r) * N;
-            for (int t = 0; t < N; t++) Bp[t] = gl_add(acc[t], gl_from_i64(gaussian(&rn, nb + t, P->glwe_sigma)));
-            uint64_t mg = s_small[i] ? g : 0;
-            row[(size_t)r * N] = gl_add(row[(size_t)r * N], mg);
+            for (int t = 0; t < N; t++)
+                Bp[t] = q_add(acc[t], q_from_i64(gaussian_s(&rn, nb + t, P->glwe_sigma, (double)Q_MOD)));
+            if (s_small[i]) row[(size_t)r * N] = q_add(row[(size_t)r * N], g);
         }
-    free(tmp); free(acc); free(S); ntt_plan_free(NP);
+    free(prod); free(acc); ntt_plan_free(NP);
 }
 
 /* ---------------------------------------------------- client encrypt/decrypt */
@@ -351,7 +378,7 @@ void or_keyswitch(const or_params* P, const uint64_t* ksk, const uint64_t* in, s
 typedef struct {
     or_params P;
     ntt_plan* NP;
-    uint64_t* bsk_ntt; /* [i][r][c][N] in the oracle's own NTT domain */
+    uint64_t* bsk_ntt[2]; /* [i][r][c][N] residues mod p_q in the oracle's own NTT domain */
 } or_bsk;
 
 void* or_bsk_prepare(const or_params* P, const uint64_t* bsk) {
@@ -359,37 +386,44 @@ void* or_bsk_prepare(const or_params* P, const uint64_t* bsk) {
     K->P = *P;
     K->NP = ntt_plan_make(P->N);
     size_t polys = (size_t)P->n * (P->k + 1) * (P->k + 1);
-    K->bsk_ntt = malloc(8 * polys * P->N);
-    memcpy(K->bsk_ntt, bsk, 8 * polys * P->N);
-    #pragma omp parallel for schedule(static)
-    for (long i = 0; i < (long)polys; i++) nega_forward(K->NP, K->bsk_ntt + (size_t)i * P->N);
+    for (int q = 0; q < 2; q++) {
+        K->bsk_ntt[q] = malloc(8 * polys * P->N);
+        memcpy(K->bsk_ntt[q], bsk, 8 * polys * P->N);
+        #pragma omp parallel for schedule(static)
+        for (long i = 0; i < (long)polys; i++) nega_forward(K->NP, q, K->bsk_ntt[q] + (size_t)i * P->N);
+    }
     return K;
 }
-void or_bsk_free(void* p) { or_bsk* K = (or_bsk*)p; ntt_plan_free(K->NP); free(K->bsk_ntt); free(K); }
+void or_bsk_free(void* p) {
+    or_bsk* K = (or_bsk*)p;
+    ntt_plan_free(K->NP); free(K->bsk_ntt[0]); free(K->bsk_ntt[1]); free(K);
+}
 
-/* LUT polynomial V (mod p): box = N/16 positions per message, recentred by half
+/* Delta = 2^59 on the torus is D_Q = 2 * round(Q / 64) in Z_Q */
+static uint64_t half_delta_q(void) { return (Q_MOD + 32) / 64; }
+/* LUT polynomial V (mod Q): box = N/16 positions per message, recentred by half
  * a box; the last half box holds -f(0) (negacyclic wrap of message 16). */
-static const uint64_t DELTA_P = (1ULL << 59) - (1ULL << 27); /* round(2^59 * p / 2^64) */
 static void make_lut_poly(int N, const uint8_t lut[16], uint64_t* V) {
+    const uint64_t dq = 2 * half_delta_q();
     int box = N / 16, half = box / 2;
     for (int j = 0; j < N; j++) {
         int m = (j + half) / box;
-        if (m < 16) V[j] = (uint64_t)lut[m] * DELTA_P;
-        else V[j] = lut[0] ? GL_P - (uint64_t)lut[0] * DELTA_P : 0;
+        if (m < 16) V[j] = (uint64_t)lut[m] * dq;
+        else V[j] = q_neg((uint64_t)lut[0] * dq);
     }
 }
 /* (X^a * poly)[j] for a in [0,2N), negacyclic */
 static inline uint64_t rot_coef(const uint64_t* poly, int N, int j, int a) {
     int s = j - a;
     s %= 2 * N; if (s < 0) s += 2 * N;
-    return s < N ? poly[s] : (poly[s - N] ? GL_P - poly[s - N] : 0);
+    return s < N ? poly[s] : q_neg(poly[s - N]);
 }
 
 /* Multi-value bootstrapping (Carpov, Izabachene, Mollimard, CT-RSA 2019):
  * with u(X) = sum_j X^j, u*(1-X) = 2 in Z[X]/(X^N+1), so every LUT polynomial
  * factors as V_f = (Delta/2) u * w_f where w_f is sparse with small integer
  * coefficients: f(m)-f(m-1) at m*box - box/2 (m = 1..15) and -(f(0)+f(15)) at
- * N - box/2.  One blind rotation of TV = (Delta_p/2) u then yields every LUT
+ * N - box/2.  One blind rotation of TV = (Delta/2) u then yields every LUT
  * on the same input: acc_f = w_f * acc (noise grows by ||w_f||_2).
  * "direct" jobs rotate V_f itself (one output, no w-step). */
 int or_lut_terms(int N, const uint8_t lut[16], int32_t* pos, int32_t* d) {
@@ -402,7 +436,7 @@ int or_lut_terms(int N, const uint8_t lut[16], int32_t* pos, int32_t* d) {
     if (dd) { pos[n] = N - half; d[n] = dd; n++; }
     return n;
 }
-/* sum_t d_t * (X^pos_t * poly)[j]  mod p */
+/* sum_t d_t * (X^pos_t * poly)[j]  mod Q */
 static uint64_t apply_w(const uint64_t* poly, int N, int j, int nt, const int32_t* pos, const int32_t* d) {
     __int128 s = 0;
     for (int t = 0; t < nt; t++) {
@@ -412,47 +446,61 @@ static uint64_t apply_w(const uint64_t* poly, int N, int j, int nt, const int32_
         else v = -(__int128)poly[src + N];
         s += v * d[t];
     }
-    s %= (__int128)GL_P;
-    if (s < 0) s += GL_P;
+    s %= (__int128)Q_MOD;
+    if (s < 0) s += Q_MOD;
     return (uint64_t)s;
 }
 
 /* Blind rotation of one keyswitched LWE, then for each of n_out LUTs the
- * w-step (unless direct), sample extract and Z_p -> 2^64 conversion. */
+ * w-step (unless direct), sample extract and Z_Q -> 2^64 conversion. */
 void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts, int n_out, int direct, uint64_t* outs) {
     or_bsk* K = (or_bsk*)pk;
     const or_params* P = &K->P;
     int k = P->k, N = P->N, n = P->n, log2N2 = ilog2(2 * N);
     size_t kp1 = (size_t)k + 1, big = (size_t)k * N;
     uint64_t* acc = calloc(kp1 * N, 8);
-    uint64_t* D = malloc(8 * kp1 * N);
-    uint64_t* res = malloc(8 * N);
+    int64_t* dig = malloc(8 * kp1 * N);
+    uint64_t* D = malloc(8 * 2 * kp1 * N);
+    uint64_t* res[2] = {malloc(8 * N), malloc(8 * N)};
     uint64_t* V = malloc(8 * N);
     /* direct == 1: the LUT polynomial itself; 0 (multi-value) and 2 (sign gate):
-     * the constant test polynomial (Delta_p/2) * sum_j X^j */
+     * the constant test polynomial (Delta/2) * sum_j X^j */
     if (direct == 1) make_lut_poly(N, luts, V);
-    else for (int j = 0; j < N; j++) V[j] = DELTA_P / 2;
+    else for (int j = 0; j < N; j++) V[j] = half_delta_q();
     uint32_t b = mod_switch(ks_lwe[n], log2N2);
     /* acc = (0, X^{-b} V) */
     for (int j = 0; j < N; j++) acc[(size_t)k * N + j] = rot_coef(V, N, j, (2 * N - (int)b) % (2 * N));
     for (int i = 0; i < n; i++) {
         uint32_t a = mod_switch(ks_lwe[i], log2N2);
         if (a == 0) continue; /* X^0 acc - acc = 0: exactly a no-op */
+        /* signed digits of (X^a - 1) * acc */
         for (size_t c = 0; c < kp1; c++) {
             const uint64_t* A = acc + c * N;
-            uint64_t* Dc = D + c * N;
-            for (int j = 0; j < N; j++) Dc[j] = or_decompose_pbs(gl_sub(rot_coef(A, N, j, (int)a), A[j]));
-            nega_forward(K->NP, Dc);
+            for (int j = 0; j < N; j++) dig[c * N + j] = decompose_q(q_sub(rot_coef(A, N, j, (int)a), A[j]));
         }
-        const uint64_t* G = K->bsk_ntt + (size_t)i * kp1 * kp1 * N;
-        for (size_t c = 0; c < kp1; c++) {
-            for (int t = 0; t < N; t++) {
-                uint64_t s = 0;
-                for (size_t r = 0; r < kp1; r++) s = gl_add(s, gl_mul(D[r * N + t], G[(r * kp1 + c) * N + t]));
-                res[t] = s;
+        /* external product per prime: NTT of the digit polynomials, MAC with
+         * the GGSW, inverse NTT; CRT and accumulate */
+        for (int q = 0; q < 2; q++) {
+            const int64_t p = (int64_t)PR[q];
+            for (size_t r = 0; r < kp1; r++) {
+                uint64_t* Dr = D + (q * kp1 + r) * N;
+                for (int j = 0; j < N; j++) Dr[j] = (uint64_t)(((dig[r * N + j] % p) + p) % p);
+                nega_forward(K->NP, q, Dr);
             }
-            nega_inverse(K->NP, res);
-            for (int t = 0; t < N; t++) acc[c * N + t] = gl_add(acc[c * N + t], res[t]);
+        }
+        for (size_t c = 0; c < kp1; c++) {
+            for (int q = 0; q < 2; q++) {
+                const uint64_t p = PR[q];
+                const uint64_t* Dq = D + q * kp1 * N;
+                const uint64_t* G = K->bsk_ntt[q] + (size_t)i * kp1 * kp1 * N;
+                for (int t = 0; t < N; t++) {
+                    uint64_t s = 0;
+                    for (size_t r = 0; r < kp1; r++) s = (s + Dq[r * N + t] * G[(r * kp1 + c) * N + t]) % p;
+                    res[q][t] = s;
+                }
+                nega_inverse(K->NP, q, res[q]);
+            }
+            for (int t = 0; t < N; t++) acc[c * N + t] = q_add(acc[c * N + t], crt2(res[0][t], res[1][t]));
         }
     }
     int32_t pos[17], d[17];
@@ -465,7 +513,7 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
             for (int t = 0; t < N; t++) {
                 int src = t == 0 ? 0 : N - t;
                 uint64_t a = direct ? A[src] : apply_w(A, N, src, nt, pos, d);
-                uint64_t v = t == 0 ? a : (a ? GL_P - a : 0);
+                uint64_t v = t == 0 ? a : q_neg(a);
                 out[(size_t)j * N + t] = or_conv(v);
             }
         }
@@ -473,7 +521,7 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
         out[big] = or_conv(direct ? B[0] : apply_w(B, N, 0, nt, pos, d));
         if (direct == 2) out[big] += 1ULL << 58; /* sign gate: +-Delta/2 + Delta/2 -> {0, Delta} */
     }
-    free(acc); free(D); free(res); free(V);
+    free(acc); free(dig); free(D); free(res[0]); free(res[1]); free(V);
 }
 
 /* single LUT, rotating the LUT polynomial itself */

@@ -36,7 +36,7 @@ def test_device_info(gctx):
 
 def test_ring_mul_bit_exact(gctx):
     rng = np.random.default_rng(1)
-    P = of.P_GOLDILOCKS
+    P = of.Q_RING
     a = rng.integers(0, P, (3, 2048), dtype=np.uint64)
     b = rng.integers(0, P, (3, 2048), dtype=np.uint64)
     b[1] = 0

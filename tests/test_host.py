@@ -126,14 +126,16 @@ def test_start_range_partition_is_or():
 
 
 def test_scalar_maps_match_oracle():
+    """Product scalar maps (Montgomery CRT, reciprocal digit, residue -> torus)
+    vs the oracle's plain 128-bit definitions."""
     L, O = F.lib(), of.lib()
-    P = of.P_GOLDILOCKS
+    Q = of.Q_RING
+    g = O.or_pbs_gadget()
     rng = np.random.default_rng(9)
-    xs = [0, 1, 2, P - 1, P - 2, (1 << 63), (1 << 41) - (1 << 9), (1 << 40) - (1 << 8), P - ((1 << 40) - (1 << 8))]
-    xs += [int(v) for v in rng.integers(0, P, 5000, dtype=np.uint64)]
+    xs = [0, 1, 2, Q - 1, Q - 2, Q // 2, Q // 2 + 1, g, g // 2, g // 2 + 1, Q - g // 2, Q - g // 2 - 1]
+    xs += [int(v) for v in rng.integers(0, Q, 5000, dtype=np.uint64)]
     for x in xs:
-        y = int(rng.integers(0, P, dtype=np.uint64))
-        assert L.fr_debug_scalar(0, x, y) == O.or_gl_mul(x, y)
+        assert L.fr_debug_scalar(0, x, 0) == x  # CRT(x mod p0, x mod p1)
         assert L.fr_debug_scalar(1, x, 0) == O.or_decompose_pbs(x)
         assert L.fr_debug_scalar(2, x, 0) == O.or_conv(x)
     dig = (ctypes.c_int32 * 5)()

@@ -64,15 +64,15 @@ def test_ring_mul_vs_schoolbook():
     L = of.lib()
     rng = np.random.default_rng(3)
     for N in (16, 256):
-        a = rng.integers(0, of.P_GOLDILOCKS, N, dtype=np.uint64)
-        b = rng.integers(0, of.P_GOLDILOCKS, N, dtype=np.uint64)
+        a = rng.integers(0, of.Q_RING, N, dtype=np.uint64)
+        b = rng.integers(0, of.Q_RING, N, dtype=np.uint64)
         o1 = np.zeros(N, np.uint64)
         o2 = np.zeros(N, np.uint64)
         L.or_ring_mul(N, of.ptr(a), of.ptr(b), of.ptr(o1))
         L.or_ring_mul_schoolbook(N, of.ptr(a), of.ptr(b), of.ptr(o2))
         assert (o1 == o2).all()
     # pure-python negacyclic product for a tiny case
-    N, P = 8, of.P_GOLDILOCKS
+    N, P = 8, of.Q_RING
     a = rng.integers(0, P, N, dtype=np.uint64)
     b = rng.integers(0, P, N, dtype=np.uint64)
     ref = [0] * N
@@ -89,20 +89,35 @@ def test_ring_mul_vs_schoolbook():
 
 
 def test_decompose_and_conv_properties():
+    """Gadget digit and Z_Q -> torus map, against their exact definitions."""
     L = of.lib()
-    P = of.P_GOLDILOCKS
-    g = (1 << 41) - (1 << 9)
+    Q = of.Q_RING
+    p0, p1 = of.RNS_PRIMES
+    assert L.or_q_modulus() == Q
+    g = L.or_pbs_gadget()
+    assert g == round(Q / 2**23) == (Q + 2**22) >> 23
     rng = np.random.default_rng(5)
-    xs = [0, 1, g // 2, g // 2 + 1, P - 1, P - 2, P - g // 2, (1 << 63), P // 2] + [int(x) for x in rng.integers(0, P, 2000, dtype=np.uint64)]
+    xs = [0, 1, g // 2, g // 2 + 1, g - 1, Q - 1, Q - 2, Q - g // 2, Q - g // 2 - 1, Q // 2, Q // 2 + 1]
+    xs += [int(x) for x in rng.integers(0, Q, 2000, dtype=np.uint64)]
+    p1m = (2**61 + p1 // 2) // p1
     for x in xs:
         d = L.or_decompose_pbs(x)
-        ds = d if d < P // 2 else d - P
-        assert -(1 << 22) <= ds < (1 << 22)
-        err = (x - ds * g) % P
-        err = err if err < P // 2 else err - P
-        assert abs(err) <= g // 2 + 1
+        ds = d if d < 2**63 else d - 2**64
+        k = (x - x % p0) // p0
+        t = (k * p1m + 2**37) >> 38
+        assert ds == (t - 2**23 if t >= 2**22 else t)
+        assert -(2**22) <= ds < 2**22
+        err = (x - ds * g) % Q  # approximate-gadget error, centred mod Q
+        err = err if err <= Q // 2 else err - Q
+        assert abs(err) <= 0.51 * g
         y = L.or_conv(x)
-        assert y == ((x << 64) + (P - 1) // 2) // P & (2**64 - 1)
+        u0 = x % p0 * pow(p1, -1, p0) % p0
+        u1 = x % p1 * pow(p0, -1, p1) % p1
+        exp = (((u0 << 64) + (p0 - 1) // 2) // p0 + ((u1 << 64) + (p1 - 1) // 2) // p1) % 2**64
+        assert y == exp
+        # within one unit of round(x * 2^64 / Q) on the torus
+        r = ((x << 64) + Q // 2) // Q % 2**64
+        assert min((y - r) % 2**64, (r - y) % 2**64) <= 1
 
 
 def test_encrypt_decrypt_roundtrip(oracle_k1):

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Build an experimental variant of libfheregex.so with extra -D flags:
+#   tools/build_variant.sh NAME [-DFOO=1 ...]  ->  fhe-regex_amd/build/exp/lib_NAME.so
+# (select it at run time with FHEREGEX_LIB=...)
+set -e
+cd "$(dirname "$0")/../fhe-regex_amd"
+make -s -j8 >/dev/null
+name=$1; shift
+mkdir -p build/exp
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -I../include -Icsrc "$@" -c csrc/device.hip -o build/exp/device_$name.o
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o build/exp/lib_$name.so build/keys.o build/regex.o build/lower.o build/capi.o build/exp/device_$name.o -lpthread
+echo "built fhe-regex_amd/build/exp/lib_$name.so"

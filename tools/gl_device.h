@@ -7,7 +7,7 @@
 #pragma once
 #include <cstdint>
 
-#include "common.h"
+#include "goldilocks.h"
 
 namespace fr {
 namespace gd {

@@ -3,7 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdint>
-#include "../fhe-regex_amd/csrc/common.h"
+#include "goldilocks.h"
 using namespace fr;
 
 template <int OP>

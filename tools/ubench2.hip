@@ -1,7 +1,7 @@
 // Cost of the non-canonical Goldilocks ops (gl_device.h) vs the canonical ones.
 #include <hip/hip_runtime.h>
 #include <cstdio>
-#include "../fhe-regex_amd/csrc/gl_device.h"
+#include "gl_device.h"
 using namespace fr;
 template <int OP>
 __global__ void __launch_bounds__(256) kern(uint64_t* out, uint64_t seed, int iters) {
