@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
     ap.add_argument("--cpu-sample", type=int, default=32, help="gate bootstraps in the CPU baseline sample (0: skip)")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
+    ap.add_argument("--halo", type=int, default=2, help="chars read past the last start (pattern span - 1; 2 for /abc/)")
     ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
     args = ap.parse_args()
 
@@ -122,9 +123,8 @@ def main():
     content = bytearray(rng.integers(0x20, 0x7F, L, dtype=np.uint8).tobytes())
     content[200:203] = b"abc"
     content = bytes(content)
-    span = 3  # chars one /abc/ branch reads
-    lo, hi = rank * args.chars, (rank + 1) * args.chars
-    win_hi = min(L, hi + span - 1)
+    lo, hi = F.shard_starts(L, world, rank)  # this rank's start offsets
+    win_hi = min(L, hi + args.halo)          # + halo: chars a branch may read past its start
     msgs = [(c >> (2 * b)) & 3 for c in content[lo:win_hi] for b in range(4)]
     blocks = ctx.encrypt_blocks(msgs, seed=7, first_block=4 * lo).reshape(win_hi - lo, 4, ctx.lwe_len)
     handles = [F.NULL_CT] * L

@@ -140,18 +140,57 @@ __device__ __forceinline__ void inv_phase(uint32_t (&x)[E], const uint32_t* zt, 
         }
     }
 }
-// LDS exchange between the layouts of phases PF and PT (row = this lane's polynomial)
+// Does the exchange between phase layouts PF and PT stay inside each wave?
+// Lane bit b of phase p holds index bit (b < lo(p) ? b : b + e); the wave
+// index is lane bits [6, log2 T).  If those map to the same index bits in both
+// layouts, every wave reads back only what it wrote.
 template <int N, int E, int PF, int PT>
+constexpr bool wave_local() {
+    using G = NttGeo<N, E>;
+    for (int b = 6; (1 << b) < G::T; ++b) {
+        const int f = b < G::lo(PF) ? b : b + G::e, t = b < G::lo(PT) ? b : b + G::e;
+        if (f != t) return false;
+    }
+    return true;
+}
+// LDS ordering inside one wave: no workgroup barrier, only a compiler fence
+// (LDS instructions of a wave execute in order).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+// LDS exchange between the layouts of phases PF and PT (row = this lane's
+// polynomial).  PRE: a barrier before writing (other waves may still read
+// these slots); the barrier after writing is dropped for wave-local exchanges.
+template <int N, int E, int PF, int PT, bool PRE = true>
 __device__ __forceinline__ void exchange(uint32_t (&x)[E], uint32_t* row, int tl) {
     using G = NttGeo<N, E>;
     uint32_t* rf = row + G::pad(G::template base<PF>(tl));
     uint32_t* rt = row + G::pad(G::template base<PT>(tl));
-    __syncthreads();
+    if constexpr (PRE) __syncthreads();
 #pragma unroll
     for (int m = 0; m < E; ++m) rf[pad_c(G::template moff<PF>(m))] = x[m];
-    __syncthreads();
+    if constexpr (wave_local<N, E, PF, PT>()) wave_sync();
+    else __syncthreads();
 #pragma unroll
     for (int m = 0; m < E; ++m) x[m] = rt[pad_c(G::template moff<PT>(m))];
+}
+
+// Barrier plan (hazards between waves on the exchange rows).  After any
+// exchange every lane reads only slots its own wave owns under the new layout,
+// and those sets partition the row; so a later write to them by the same
+// wave cannot race another wave.  Only the first exchange of an NTT needs a
+// barrier before writing: the forward one follows the rotation step (other
+// waves read arbitrary slots of this row), the inverse one follows the MAC
+// (other polynomials' waves read this row).
+template <int N, int E, int p>
+constexpr bool fwd_pre() {
+    return p == 0;
+}
+template <int N, int E, int p>
+constexpr bool inv_pre() {
+    return p == NttGeo<N, E>::NPH - 1;
 }
 
 template <int N, int E, int p>
@@ -159,7 +198,7 @@ __device__ __forceinline__ void forward_from(uint32_t (&x)[E], uint32_t* row, co
                                              uint32_t pn) {
     fwd_phase<N, E, p>(x, zt, tl, pm, pn);
     if constexpr (p + 1 < NttGeo<N, E>::NPH) {
-        exchange<N, E, p, p + 1>(x, row, tl);
+        exchange<N, E, p, p + 1, fwd_pre<N, E, p>()>(x, row, tl);
         forward_from<N, E, p + 1>(x, row, zt, tl, pm, pn);
     }
 }
@@ -168,7 +207,7 @@ __device__ __forceinline__ void inverse_from(uint32_t (&x)[E], uint32_t* row, co
                                              uint32_t pn) {
     inv_phase<N, E, p>(x, zt, tl, pm, pn);
     if constexpr (p > 0) {
-        exchange<N, E, p, p - 1>(x, row, tl);
+        exchange<N, E, p, p - 1, inv_pre<N, E, p>()>(x, row, tl);
         inverse_from<N, E, p - 1>(x, row, zt, tl, pm, pn);
     }
 }
@@ -192,7 +231,8 @@ constexpr int br_threads() {
 }
 template <int N, int K, int E>
 constexpr size_t br_smem_bytes() {
-    return sizeof(uint32_t) * (2 * (size_t)(K + 1) * NttGeo<N, E>::NP + 2 * (size_t)N) + 16 * MAX_OUT + 2 * 1024;
+    return sizeof(uint32_t) * (2 * (size_t)(K + 1) * NttGeo<N, E>::NP + 2 * (size_t)N) + 16 * MAX_OUT + 2 * 1024 +
+           4 * 17 * MAX_OUT;
 }
 
 // BSK NTT-domain layout [i][r][c][prime][slot]: natural (bit-reversed) slot
@@ -214,25 +254,36 @@ constexpr int br_min_waves() {
     return E == 16 ? FR_BR_MINW16 : FR_BR_MINW8;
 }
 
-// (x_0, x_1) residues of sum_t d_t (X^pos_t A)[j] for the multi-value w-step
+// Multi-value w-step terms of one LUT: w_f = sum_t d_t X^pos_t with
+// d = f(m) - f(m-1) at m*box - box/2 and -(f(0) + f(15)) at N - box/2.
+// Packed as pos | (d + 128) << 16; returns the count.
 template <int N>
-__device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint8_t* lf, int j, uint32_t pm, int q) {
+__device__ __forceinline__ int lut_terms(const uint8_t* lf, uint32_t* terms) {
     constexpr int box = N / 16, half = box / 2;
-    uint64_t pos = 0, neg = 0;
+    int nt = 0;
     for (int tt = 1; tt <= 16; ++tt) {
-        int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
-        if (d == 0) continue;  // uniform across the workgroup
-        int src = j - (tt < 16 ? tt * box - half : N - half);
+        const int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+        if (d != 0) terms[nt++] = (uint32_t)(tt < 16 ? tt * box - half : N - half) | ((uint32_t)(d + 128) << 16);
+    }
+    return nt;
+}
+// residue of sum_t d_t (X^pos_t A)[j] mod p from one residue row of A
+template <int N>
+__device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint32_t* terms, int nt, int j, uint32_t pm,
+                                           int q) {
+    int64_t acc = 0;
+    for (int t = 0; t < nt; ++t) {  // nt uniform, terms broadcast from LDS
+        const uint32_t tm = terms[t];
+        int src = j - (int)(tm & 0xFFFF);
+        int d = (int)(tm >> 16) - 128;
         if (src < 0) {
             src += N;
             d = -d;
         }
-        const uint64_t v = row[lds_pad(src)];
-        if (d > 0) pos += v * (uint64_t)d;
-        else neg += v * (uint64_t)(-d);
+        acc += (int64_t)d * (int64_t)row[lds_pad(src)];
     }
-    // |sum| < 16 * 30 * p: shift by 512p before reducing
-    return rns::reduce64(pos + 512ULL * pm - neg, q);
+    // |acc| < 16 * 30 * p: shift by 512p before reducing
+    return rns::reduce64((uint64_t)(acc + 512LL * pm), q);
 }
 
 template <int N, int K, int E>
@@ -248,6 +299,8 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     uint32_t* zt_all = xbuf + 2 * (K + 1) * G::NP;       // 2 x N Montgomery twiddles
     uint8_t* lut = (uint8_t*)(zt_all + 2 * N);           // 16 * n_out
     uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);    // n (<= 1024)
+    uint32_t* wterms = (uint32_t*)(abar + 1024);          // multi-value terms, 16 per output
+    int* wcnt = (int*)(wterms + 16 * MAX_OUT);
 
     const int tid = threadIdx.x;
     const int PQ = __builtin_amdgcn_readfirstlane(tid / G::T), tl = tid % G::T;  // wave-uniform
@@ -292,15 +345,14 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             }
         }
         __syncthreads();
+        const bool body = P == K;  // mask rows start at zero
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            acc[m] = 0;
-            if (P == K) {
-                const int s = (b0 + G::template moff<0>(m) + (int)bbar) & (2 * N - 1);
-                const uint32_t v = row[G::pad(s & (N - 1))];
-                acc[m] = s < N ? v : rns::negm(v, pm);
-            }
+            const int s = (b0 + G::template moff<0>(m) + (int)bbar) & (2 * N - 1);
+            const uint32_t v = row[G::pad(s & (N - 1))];
+            acc[m] = body ? (s < N ? v : rns::negm(v, pm)) : 0u;
         }
+        __syncthreads();  // the rotated reads above touch slots other waves write next
     }
 
     const size_t ggsw = (size_t)(K + 1) * (K + 1) * 2 * N;
@@ -319,7 +371,8 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         }
         // 1. (X^a - 1) * acc, CRT of the two residues, signed gadget digit
         uint32_t x[E];
-        __syncthreads();
+        // (no barrier before the write: the last inverse exchange left these
+        // slots read by this wave only)
 #pragma unroll
         for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
         __syncthreads();
@@ -340,7 +393,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         // 2. forward NTT of this lane group's digit residues
         forward_ntt<N, E>(x, row, zt, tl, pm, pn);
         // 3. external product MAC (in place): x_(P,q) = sum_r D_(r,q) * GGSW_i[r][P][q]
-        __syncthreads();
+        //    (no barrier before the write: these slots were last read by this wave)
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
         __syncthreads();
@@ -386,14 +439,17 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         return;
     }
     // multi-value: acc_f = w_f * acc with w_f = sum_t d_t X^{pos_t} (small d_t)
+    if (tid < n_out) wcnt[tid] = lut_terms<N>(lut + 16 * tid, wterms + 16 * tid);
+    __syncthreads();
     for (int f = 0; f < n_out; ++f) {
-        const uint8_t* lf = lut + 16 * f;
+        const uint32_t* tf = wterms + 16 * f;
+        const int nt = wcnt[f];
         uint64_t* out = arena + (size_t)gates[g].out_slot[f] * slot_stride;
         for (int c = tid; c <= big; c += NT) {
             const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
             const int j = t == 0 ? 0 : N - t;
             const uint32_t* r0 = xbuf + 2 * pp * G::NP;
-            uint32_t v0 = w_step<N>(r0, lf, j, rns::P0, 0), v1 = w_step<N>(r0 + G::NP, lf, j, rns::P1, 1);
+            uint32_t v0 = w_step<N>(r0, tf, nt, j, rns::P0, 0), v1 = w_step<N>(r0 + G::NP, tf, nt, j, rns::P1, 1);
             if (t != 0) {
                 v0 = rns::negm(v0, rns::P0);
                 v1 = rns::negm(v1, rns::P1);

@@ -20,7 +20,7 @@ from __future__ import annotations
 import ctypes as C
 import os
 from dataclasses import dataclass
-from typing import List, Optional, Sequence
+from typing import Tuple, List, Optional, Sequence
 
 import numpy as np
 
@@ -412,6 +412,20 @@ def has_match(sk: ServerKey, content: Sequence[int], pattern: str) -> int:
     """engine.rs:8-42: returns the encrypted 0/1 result handle."""
     out, _ = sk.ctx.has_match(content, pattern)
     return out
+
+
+def shard_starts(L: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous range [lo, hi) of start offsets owned by `rank`.
+
+    The reference's driver ORs one branch set per start offset
+    (engine.rs:22-35); offsets are independent, so ranks split them into
+    contiguous ranges, evaluate their OR tree locally (fr_has_match_range) and
+    a final OR over the gathered per-rank booleans gives the full result."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    base, extra = divmod(L, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
 
 
 def header_symbols() -> List[str]:

@@ -100,12 +100,13 @@ int fr_default_params(fr_params* out); /* PARAM_MESSAGE_2_CARRY_2, k=1, N=2048 *
 /* ----- keys ----- */
 /* bincode RadixClientKey (tfhe-rs 0.2 layout, reference test_data/client_key). */
 int fr_load_client_key(fr_ctx* ctx, const uint8_t* bincode, size_t len);
-/* Deterministic server key (KSK mod 2^64, BSK mod p) from the client key and a
+/* Deterministic server key (KSK mod 2^64, BSK mod Q) from the client key and a
  * seed (ServerKey::new, engine.rs:252); uploads it and converts the BSK to the
  * NTT domain on the device when the context has one. */
 int fr_gen_server_key(fr_ctx* ctx, uint64_t seed);
 /* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = n*(k+1)^2*N u64
- * (coefficient domain mod p, layout [i][row][component][coef]).  Either may be NULL. */
+ * (coefficient domain mod Q = 998244353*1004535809, layout [i][row][component][coef]).
+ * Either may be NULL. */
 int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
 int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len);
 

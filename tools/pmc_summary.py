@@ -1,0 +1,68 @@
+"""Summarise rocprofv3 PMC passes (tools/profile.sh output) for the BR kernel.
+
+HBM bytes per launch = (FETCH_SIZE x 2 + WRITE_SIZE) KiB x 1024, with the gfx950
+FETCH_SIZE correction (x2 for 16-B-per-lane streaming reads,
+MI355X_MICROARCH.md HBM section).  Launches are grouped by grid size; the
+per-match average over the blind-rotation launches of one has_match is what
+bench.py reports as roofline.traffic.
+Usage: python3 tools/pmc_summary.py PROFDIR OUT.json
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def load(d, name):
+    p = os.path.join(d, name, "run_counter_collection.csv")
+    rows = list(csv.DictReader(open(p)))
+    out = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in rows:
+        k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        out[(k, int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    return out
+
+
+def main():
+    d, out_path = sys.argv[1], sys.argv[2]
+    fetch, write = load(d, "pmc_fetch"), load(d, "pmc_write")
+    sq, lds = load(d, "pmc_sq"), load(d, "pmc_lds")
+    launches = []
+    for key in sorted(fetch):
+        k, grid = key
+        if "blind_rotate" not in k:
+            continue
+        f = fetch[key]["FETCH_SIZE"]
+        w = write.get(key, {}).get("WRITE_SIZE", [0.0])
+        ent = {"kernel": k, "grid": grid, "calls": len(f),
+               "fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
+        ent["hbm_bytes"] = ent["fetch_bytes"] + ent["write_bytes"]
+        s = sq.get(key, {})
+        if s:
+            avg = {c: sum(v) / len(v) for c, v in s.items()}
+            wc = avg.get("SQ_WAVE_CYCLES", 0) or 1
+            ent["wave_cycle_split"] = {"active": avg.get("SQ_ACTIVE_INST_ANY", 0) / wc,
+                                       "issue_stall": avg.get("SQ_WAIT_INST_ANY", 0) / wc,
+                                       "parked": avg.get("SQ_WAIT_ANY", 0) / wc}
+            ent["valu_insts"] = avg.get("SQ_INSTS_VALU")
+        l = lds.get(key, {})
+        if l:
+            avg = {c: sum(v) / len(v) for c, v in l.items()}
+            ent["lds_bank_conflict_cycles"] = avg.get("SQ_LDS_BANK_CONFLICT")
+            ent["lds_insts"] = avg.get("SQ_INSTS_LDS")
+            ent["grbm_gui_active_per_xcd"] = avg.get("GRBM_GUI_ACTIVE", 0) / 8
+        launches.append(ent)
+    # one has_match = the launches of the four levels; the saturated probe is the biggest grid
+    sat = max(launches, key=lambda e: e["grid"]) if launches else None
+    match = [e for e in launches if e is not sat]
+    per_launch = sum(e["hbm_bytes"] * e["calls"] for e in match) / max(1, sum(e["calls"] for e in match))
+    res = {"hbm_bytes_per_launch": per_launch, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the /abc/ match, averaged per launch",
+           "launches": launches}
+    with open(out_path, "w") as f:
+        json.dump(res, f, indent=1)
+    print(json.dumps({"hbm_bytes_per_launch": per_launch}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
