@@ -83,7 +83,7 @@ def main():
     ap.add_argument("--pattern", default="/abc/")
     ap.add_argument("--params", default="k1n2048", choices=["k1n2048", "k2n1024"])
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
-    ap.add_argument("--cpu-sample", type=int, default=32, help="gate bootstraps in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=384, help="gate bootstraps in the CPU baseline sample (0: skip)")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
     ap.add_argument("--halo", type=int, default=2, help="chars read past the last start (pattern span - 1; 2 for /abc/)")
     ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
