@@ -440,7 +440,7 @@ int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len) {
         NEED(ctx);
         const Params& p = ctx->p;
         if (ksk_len) *ksk_len = (size_t)p.big() * p.ks_level * (p.n + 1);
-        if (bsk_len) *bsk_len = (size_t)p.n * (p.k + 1) * (p.k + 1) * p.N;
+        if (bsk_len) *bsk_len = p.bsk_len();
     })
 }
 

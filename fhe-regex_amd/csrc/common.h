@@ -66,6 +66,11 @@ struct Params {
     int slot_stride() const { return (lwe_len() + 7) & ~7; }
     int ks_stride() const { return (n + 1 + 7) & ~7; }
     int log2N() const { int l = 0; while ((1 << l) < N) ++l; return l; }
+    // bootstrapping-key unrolling: k = 1 processes LWE coefficients in pairs
+    // (3 GGSWs per pair: s_i s_j, s_i(1-s_j), (1-s_i)s_j); k > 1 one GGSW each
+    int bsk_unroll() const { return k == 1 ? 2 : 1; }
+    size_t bsk_ggsw() const { return bsk_unroll() == 2 ? 3 * (size_t)((n + 1) / 2) : (size_t)n; }
+    size_t bsk_len() const { return bsk_ggsw() * (size_t)(k + 1) * (k + 1) * N; }
 };
 Params params_from_c(const fr_params* p);
 void validate_params(const Params& p);

@@ -229,11 +229,17 @@ template <int N, int K, int E>
 constexpr int br_threads() {
     return 2 * (K + 1) * (N / E);
 }
+// bootstrapping-key unrolling factor (Params::bsk_unroll): pairs for k = 1
+template <int K>
+constexpr int br_unroll() {
+    return K == 1 ? 2 : 1;
+}
 template <int N, int K, int E>
 constexpr size_t br_smem_bytes() {
-    return sizeof(uint32_t) * (2 * (size_t)(K + 1) * NttGeo<N, E>::NP + 2 * (size_t)N) + 16 * MAX_OUT + 2 * 1024 +
-           4 * 17 * MAX_OUT;
+    return sizeof(uint32_t) * (2 * (size_t)(K + 1) * NttGeo<N, E>::NP + 2 * (size_t)N) + 16 * MAX_OUT + 2 * 1026 +
+           4 * 17 * MAX_OUT + (br_unroll<K>() == 2 ? sizeof(uint32_t) * 4 * (size_t)N : 0);
 }
+constexpr int brv_c(int x, int bits) { return bits == 0 ? 0 : ((x & 1) << (bits - 1)) | brv_c(x >> 1, bits - 1); }
 
 // BSK NTT-domain layout [i][r][c][prime][slot]: natural (bit-reversed) slot
 // order, the same for every lane geometry E, so E can be chosen per launch.
@@ -298,9 +304,11 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     uint32_t* xbuf = smem;                                // 2(K+1) rows of NP: row (P, q) at (2P + q) * NP
     uint32_t* zt_all = xbuf + 2 * (K + 1) * G::NP;       // 2 x N Montgomery twiddles
     uint8_t* lut = (uint8_t*)(zt_all + 2 * N);           // 16 * n_out
-    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);    // n (<= 1024)
-    uint32_t* wterms = (uint32_t*)(abar + 1024);          // multi-value terms, 16 per output
+    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);    // n (<= 1024), zero-padded to even
+    uint32_t* wterms = (uint32_t*)(abar + 1026);          // multi-value terms, 16 per output
     int* wcnt = (int*)(wterms + 16 * MAX_OUT);
+    uint32_t* mono = (uint32_t*)(wcnt + MAX_OUT);         // unrolled: (psi^e - 1) * R per prime, e < 2N
+    constexpr int U = br_unroll<K>();
 
     const int tid = threadIdx.x;
     const int PQ = __builtin_amdgcn_readfirstlane(tid / G::T), tl = tid % G::T;  // wave-uniform
@@ -315,7 +323,19 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     for (int i = tid; i < 2 * N; i += NT) zt_all[i] = tw[i];
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], G::LOG + 1);
+    if (tid == 0) abar[n] = 0;  // pad an odd n
     const uint32_t bbar = mod_switch(in[n], G::LOG + 1);
+    if constexpr (U == 2) {
+        __syncthreads();  // twiddles loaded
+        // X^e in the NTT domain is psi^(e(2 brv(slot) + 1)); psi^e = +-zeta[brv(e mod N)]
+        for (int i = tid; i < 4 * N; i += NT) {
+            const int qq = i / (2 * N), e = i % (2 * N);
+            const uint32_t pq = rns::prime(qq);
+            const uint32_t z = zt_all[qq * N + (int)(__brev((uint32_t)(e & (N - 1))) >> (32 - G::LOG))];
+            const uint32_t v = e < N ? z : rns::negm(z, pq);
+            mono[i] = rns::subm(v, (uint32_t)((1ULL << 32) % pq), pq);  // (psi^e - 1) * 2^32 mod p
+        }
+    }
     __syncthreads();
     const uint32_t* zt = zt_all + q * N;
 
@@ -356,6 +376,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     }
 
     const size_t ggsw = (size_t)(K + 1) * (K + 1) * 2 * N;
+    if constexpr (U == 1) {
     for (int i = 0; i < n; ++i) {
         const int a = abar[i];
         if (a == 0) continue;  // X^0*acc - acc = 0: exact no-op (uniform branch)
@@ -412,6 +433,74 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
 #pragma unroll
         for (int m = 0; m < E; ++m) acc[m] = red1(red1(x[m], pm) + acc[m], pm);
+    }
+    } else {
+    // Unrolled blind rotation: one step per pair (i, j) = (2t, 2t+1),
+    //   acc += sum_g (X^e_g - 1) * (GGSW_3t+g [x] acc),  e = (a_i + a_j, a_i, a_j),
+    // with one decomposition of acc, one forward NTT per polynomial, the three
+    // monomial factors applied slot-wise in the NTT domain, one inverse NTT.
+    const uint32_t* sib_b0 = xbuf + (2 * P + (1 - q)) * G::NP + G::pad(b0);  // other prime, same polynomial
+    const uint32_t* mono_q = mono + q * 2 * N;
+    const uint32_t B0 = 2 * (__brev((uint32_t)bl) >> (32 - G::LOG)) + 1;  // slot bl + moff: 2 brv + 1 = B0 + c_m
+    const int steps = (n + 1) / 2;
+    for (int t = 0; t < steps; ++t) {
+        const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
+        if ((ai | aj) == 0) continue;  // X^0*acc - acc = 0 (uniform branch)
+        // 0. prefetch the three GGSWs of this pair
+        uint32_t gv[3][K + 1][E];
+        {
+            const uint32_t* gi = bsk + (size_t)(3 * t) * ggsw + (size_t)(P * 2 + q) * N + bl;
+#pragma unroll
+            for (int gg = 0; gg < 3; ++gg)
+#pragma unroll
+                for (int r = 0; r <= K; ++r)
+#pragma unroll
+                    for (int m = 0; m < E; ++m)
+                        gv[gg][r][m] = gi[(size_t)gg * ggsw + (size_t)r * (K + 1) * 2 * N + G::template moff<LAST>(m)];
+        }
+        // 1. signed gadget digits of acc (the other prime's residue through LDS)
+        uint32_t x[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const uint32_t o = sib_b0[pad_c(G::template moff<0>(m))];
+            const int32_t dg = q ? rns::decompose(o, acc[m]) : rns::decompose(acc[m], o);
+            x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
+        }
+        // 2. forward NTT (its first exchange waits for the sibling reads above)
+        forward_ntt<N, E>(x, row, zt, tl, pm, pn);
+        // 3. MAC with the three GGSWs and their monomial factors
+#pragma unroll
+        for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
+        __syncthreads();
+        const uint32_t e[3] = {(ai + aj) & (2 * N - 1), ai, aj};
+        uint32_t eb[3];
+#pragma unroll
+        for (int gg = 0; gg < 3; ++gg) eb[gg] = __builtin_amdgcn_readfirstlane(e[gg]) * B0;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int po = pad_c(G::template moff<LAST>(m));
+            uint32_t d[K + 1];
+#pragma unroll
+            for (int r = 0; r <= K; ++r) d[r] = (r == P) ? x[m] : xbuf_q_bl[2 * r * G::NP + po];
+            uint32_t z = 0;
+#pragma unroll
+            for (int gg = 0; gg < 3; ++gg) {
+                uint32_t y = 0;
+#pragma unroll
+                for (int r = 0; r <= K; ++r) y = red2(y + mont_lazy_d(d[r], gv[gg][r][m], pm, pn), pm);
+                const uint32_t ex = (eb[gg] + e[gg] * (uint32_t)(2 * brv_c(G::template moff<LAST>(m), G::LOG))) & (2 * N - 1);
+                z = red2(z + mont_lazy_d(y, mono_q[ex], pm, pn), pm);
+            }
+            x[m] = z;  // [0, 2p)
+        }
+        // 4. inverse NTT and accumulate (1/N is folded into the BSK)
+        inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
+#pragma unroll
+        for (int m = 0; m < E; ++m) acc[m] = red1(red1(x[m], pm) + acc[m], pm);
+    }
     }
 
     // publish the accumulator: the outputs need both residues of a coefficient
@@ -675,6 +764,8 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         HIP_CHECK(hipEventCreate(&ev));
         e = ev;
     }
+    // unrolled (k = 1) kernels keep three GGSW rows in registers: E = 8 only
+    if (p.bsk_unroll() == 2) e_ = e_small_ = 8;
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
@@ -774,9 +865,8 @@ void Device::zero_slot(int slot) {
 }
 
 void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk) {
-    const size_t kp1 = p_.k + 1;
     if (ksk.size() != (size_t)p_.big() * p_.ks_level * (p_.n + 1)) throw Error(FR_ERR_INVALID, "ksk size");
-    if (bsk.size() != (size_t)p_.n * kp1 * kp1 * p_.N) throw Error(FR_ERR_INVALID, "bsk size");
+    if (bsk.size() != p_.bsk_len()) throw Error(FR_ERR_INVALID, "bsk size");
     (void)hipFree(d_ksk_);
     (void)hipFree(d_bsk_);
     d_ksk_ = nullptr;
@@ -799,7 +889,7 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
         }
         ninv_r[q] = (uint32_t)((inv << 32) % pq);
     }
-    const int blocks = p_.n * (p_.k + 1);
+    const int blocks = (int)p_.bsk_ggsw() * (p_.k + 1);
     dispatch(p_, e_, [&](auto n_, auto k_, auto e_c) {
         constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
         k_bsk_to_ntt<N, K, E><<<blocks, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(coef, d_tw_, ninv_r[0],

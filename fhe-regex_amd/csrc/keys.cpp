@@ -237,10 +237,18 @@ void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
     });
 }
 
+// message bit of GGSW number w (see Params::bsk_unroll)
+static uint64_t ggsw_msg(const Params& p, const ClientKey& ck, size_t w) {
+    if (p.bsk_unroll() == 1) return ck.s_small[w];
+    const size_t t = w / 3, g = w % 3, i = 2 * t, j = 2 * t + 1;
+    const uint64_t si = ck.s_small[i], sj = j < (size_t)p.n ? ck.s_small[j] : 0;
+    return g == 0 ? (si & sj) : g == 1 ? (si & (1 - sj)) : ((1 - si) & sj);
+}
+
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk) {
-    const int k = p.k, N = p.N, n = p.n;
-    const size_t kp1 = (size_t)k + 1;
-    bsk.assign((size_t)n * kp1 * kp1 * N, 0);
+    const int k = p.k, N = p.N;
+    const size_t kp1 = (size_t)k + 1, nw = p.bsk_ggsw();
+    bsk.assign(p.bsk_len(), 0);
     NttTables T(N);
     // NTT of the key polynomials S_j, per prime
     std::vector<uint32_t> S[2];
@@ -251,9 +259,10 @@ void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
             T.forward(q, S[q].data() + (size_t)j * N);
         }
     }
-    parallel_for(n, [&](int i) {
+    parallel_for((int)nw, [&](int i) {
         Rng rm(seed, STREAM_BSK_MASK), rn(seed, STREAM_BSK_NOISE);
         std::vector<uint32_t> tmp(N), acc[2] = {std::vector<uint32_t>(N), std::vector<uint32_t>(N)};
+        const uint64_t msg = ggsw_msg(p, ck, (size_t)i);
         for (size_t r = 0; r < kp1; ++r) {
             uint64_t* row = bsk.data() + ((size_t)i * kp1 + r) * kp1 * N;
             std::fill(acc[0].begin(), acc[0].end(), 0);
@@ -277,7 +286,7 @@ void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
             uint64_t nb = ((uint64_t)i * kp1 + r) * N;
             for (int t = 0; t < N; ++t)
                 Bp[t] = q_add(rns::crt(acc[0][t], acc[1][t]), zq_from_i64(rn.gaussian(nb + t, p.glwe_sigma, (double)Q)));
-            if (ck.s_small[i]) row[r * N] = q_add(row[r * N], rns::G);
+            if (msg) row[r * N] = q_add(row[r * N], rns::G);
         }
     });
 }

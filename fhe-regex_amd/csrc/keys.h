@@ -49,7 +49,8 @@ ClientKey parse_client_key(const uint8_t* data, size_t len);
 
 // KSK: [i in kN][level j][t in n+1], torus 2^64.
 void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& ksk);
-// BSK: [i in n][row r in k+1][component c in k+1][coef], coefficient domain mod Q (rns.h).
+// BSK: [GGSW w][row r in k+1][component c in k+1][coef], coefficient domain mod Q (rns.h);
+// GGSW w per Params::bsk_unroll (k = 1: 3 per pair of LWE coefficients).
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk);
 
 // Fresh LWE encryptions of block messages (Delta = 2^59) under the big key.

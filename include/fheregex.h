@@ -104,9 +104,11 @@ int fr_load_client_key(fr_ctx* ctx, const uint8_t* bincode, size_t len);
  * seed (ServerKey::new, engine.rs:252); uploads it and converts the BSK to the
  * NTT domain on the device when the context has one. */
 int fr_gen_server_key(fr_ctx* ctx, uint64_t seed);
-/* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = n*(k+1)^2*N u64
- * (coefficient domain mod Q = 998244353*1004535809, layout [i][row][component][coef]).
- * Either may be NULL. */
+/* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = W*(k+1)^2*N u64
+ * (coefficient domain mod Q = 998244353*1004535809, layout [w][row][component][coef]).
+ * k = 1: bootstrapping-key unrolling, W = 3*ceil(n/2) GGSWs, w = 3t+g encrypts
+ * s_2t*s_2t+1, s_2t*(1-s_2t+1), (1-s_2t)*s_2t+1 for g = 0, 1, 2; k > 1: W = n,
+ * GGSW w encrypts s_w.  Sizes from fr_server_key_sizes.  Either may be NULL. */
 int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
 int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len);
 

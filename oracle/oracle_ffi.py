@@ -75,6 +75,9 @@ def lib():
         L.or_mod_switch.argtypes = [C.c_uint64, C.c_int]
         L.or_keygen_ksk.argtypes = [C.POINTER(Params), u64p, u64p, C.c_uint64, u64p]
         L.or_keygen_bsk.argtypes = [C.POINTER(Params), u64p, u64p, C.c_uint64, u64p]
+        L.or_bsk_len.restype = C.c_size_t
+        L.or_bsk_len.argtypes = [C.POINTER(Params)]
+        L.or_bsk_unroll.argtypes = [C.POINTER(Params)]
         L.or_encrypt.argtypes = [C.POINTER(Params), u64p, C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64, C.c_uint64, u64p]
         L.or_phase.argtypes = [C.c_int, u64p, u64p, C.c_size_t, u64p]
         L.or_decode16.restype = C.c_uint32
@@ -154,8 +157,7 @@ class Oracle:
         self.bsk = None
         self._pk = None
         if with_bsk:
-            kp1 = self.P.k + 1
-            self.bsk = np.zeros(self.n * kp1 * kp1 * self.P.N, dtype=np.uint64)
+            self.bsk = np.zeros(L.or_bsk_len(C.byref(self.P)), dtype=np.uint64)
             L.or_keygen_bsk(C.byref(self.P), ptr(self.s_big), ptr(self.s_small), seed, ptr(self.bsk))
             self._pk = L.or_bsk_prepare(C.byref(self.P), ptr(self.bsk))
 

@@ -292,17 +292,37 @@ void or_keygen_ksk(const or_params* P, const uint64_t* s_big, const uint64_t* s_
         }
 }
 
-/* BSK in the coefficient domain mod Q; layout [i][r][c][t], r,c in [0,k].
- * GGSW row r of s_small[i]: a GLWE encryption of zero (mask uniform in Z_Q,
- * body = sum_j A_j S_j + e) plus g * s_small[i] on component r. */
+/* Bootstrapping-key unrolling (pairs of LWE coefficients per blind-rotation
+ * step, k = 1): GGSW number w = 3t + g encrypts, for i = 2t, j = 2t+1,
+ *   g = 0: s_i s_j,  g = 1: s_i (1 - s_j),  g = 2: (1 - s_i) s_j
+ * (s_j = 0 past the end), so that X^(a_i s_i + a_j s_j) - 1 =
+ * sum_g m_g (X^(e_g) - 1) with e = (a_i + a_j, a_i, a_j).  k > 1: one GGSW
+ * of s_i per coefficient (no unrolling). */
+static int bsk_unroll(const or_params* P) { return P->k == 1 ? 2 : 1; }
+static size_t bsk_ggsw(const or_params* P) {
+    return bsk_unroll(P) == 2 ? 3 * (size_t)((P->n + 1) / 2) : (size_t)P->n;
+}
+size_t or_bsk_len(const or_params* P) { return bsk_ggsw(P) * (size_t)(P->k + 1) * (P->k + 1) * P->N; }
+int or_bsk_unroll(const or_params* P) { return bsk_unroll(P); }
+static uint64_t ggsw_msg(const or_params* P, const uint64_t* s_small, size_t w) {
+    if (bsk_unroll(P) == 1) return s_small[w];
+    size_t t = w / 3, g = w % 3, i = 2 * t, j = 2 * t + 1;
+    uint64_t si = s_small[i], sj = j < (size_t)P->n ? s_small[j] : 0;
+    return g == 0 ? (si & sj) : g == 1 ? (si & (1 - sj)) : ((1 - si) & sj);
+}
+
+/* BSK in the coefficient domain mod Q; layout [w][r][c][t], r,c in [0,k].
+ * GGSW row r of message m_w: a GLWE encryption of zero (mask uniform in Z_Q,
+ * body = sum_j A_j S_j + e) plus g * m_w on component r. */
 void or_keygen_bsk(const or_params* P, const uint64_t* s_big, const uint64_t* s_small, uint64_t seed, uint64_t* bsk) {
-    int k = P->k, N = P->N, n = P->n;
+    int k = P->k, N = P->N;
     const uint64_t g = pbs_g();
+    const size_t nw = bsk_ggsw(P);
     ntt_plan* NP = ntt_plan_make(N);
     rng_t rm = rng_make(seed, STREAM_BSK_MASK), rn = rng_make(seed, STREAM_BSK_NOISE);
     uint64_t* prod = malloc(8 * (size_t)N);
     uint64_t* acc = malloc(8 * (size_t)N);
-    for (int i = 0; i < n; i++)
+    for (size_t i = 0; i < nw; i++)
         for (int r = 0; r <= k; r++) {
             uint64_t* row = bsk + ((size_t)i * (k + 1) + r) * (k + 1) * N;
             for (int t = 0; t < N; t++) acc[t] = 0;
@@ -317,7 +337,7 @@ void or_keygen_bsk(const or_params* P, const uint64_t* s_big, const uint64_t* s_
             uint64_t nb = ((uint64_t)i * (k + 1) + r) * N;
             for (int t = 0; t < N; t++)
                 Bp[t] = q_add(acc[t], q_from_i64(gaussian_s(&rn, nb + t, P->glwe_sigma, (double)Q_MOD)));
-            if (s_small[i]) row[(size_t)r * N] = q_add(row[(size_t)r * N], g);
+            if (ggsw_msg(P, s_small, i)) row[(size_t)r * N] = q_add(row[(size_t)r * N], g);
         }
     free(prod); free(acc); ntt_plan_free(NP);
 }
@@ -385,7 +405,7 @@ void* or_bsk_prepare(const or_params* P, const uint64_t* bsk) {
     or_bsk* K = (or_bsk*)calloc(1, sizeof(or_bsk));
     K->P = *P;
     K->NP = ntt_plan_make(P->N);
-    size_t polys = (size_t)P->n * (P->k + 1) * (P->k + 1);
+    size_t polys = bsk_ggsw(P) * (P->k + 1) * (P->k + 1);
     for (int q = 0; q < 2; q++) {
         K->bsk_ntt[q] = malloc(8 * polys * P->N);
         memcpy(K->bsk_ntt[q], bsk, 8 * polys * P->N);
@@ -463,6 +483,7 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
     uint64_t* D = malloc(8 * 2 * kp1 * N);
     uint64_t* res[2] = {malloc(8 * N), malloc(8 * N)};
     uint64_t* V = malloc(8 * N);
+    uint64_t* Y = malloc(8 * N);
     /* direct == 1: the LUT polynomial itself; 0 (multi-value) and 2 (sign gate):
      * the constant test polynomial (Delta/2) * sum_j X^j */
     if (direct == 1) make_lut_poly(N, luts, V);
@@ -470,16 +491,23 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
     uint32_t b = mod_switch(ks_lwe[n], log2N2);
     /* acc = (0, X^{-b} V) */
     for (int j = 0; j < N; j++) acc[(size_t)k * N + j] = rot_coef(V, N, j, (2 * N - (int)b) % (2 * N));
-    for (int i = 0; i < n; i++) {
-        uint32_t a = mod_switch(ks_lwe[i], log2N2);
-        if (a == 0) continue; /* X^0 acc - acc = 0: exactly a no-op */
-        /* signed digits of (X^a - 1) * acc */
+    const int U = bsk_unroll(P);
+    for (int i = 0; i < n; i += U) {
+        /* step over coefficients i .. i+U-1: exponents of the U (or 2^U - 1) terms */
+        uint32_t ai = mod_switch(ks_lwe[i], log2N2);
+        uint32_t aj = (U == 2 && i + 1 < n) ? mod_switch(ks_lwe[i + 1], log2N2) : 0;
+        if (ai == 0 && aj == 0) continue; /* X^0 acc - acc = 0: exactly a no-op */
+        uint32_t e[3];
+        int nterms = U == 2 ? 3 : 1;
+        if (U == 2) { e[0] = (ai + aj) % (2 * (uint32_t)N); e[1] = ai; e[2] = aj; }
+        /* signed digits of the decomposed polynomial: (X^a - 1) * acc (plain
+         * CMUX) or acc itself (unrolled: the monomials multiply afterwards) */
         for (size_t c = 0; c < kp1; c++) {
             const uint64_t* A = acc + c * N;
-            for (int j = 0; j < N; j++) dig[c * N + j] = decompose_q(q_sub(rot_coef(A, N, j, (int)a), A[j]));
+            for (int j = 0; j < N; j++)
+                dig[c * N + j] = decompose_q(U == 2 ? A[j] : q_sub(rot_coef(A, N, j, (int)ai), A[j]));
         }
-        /* external product per prime: NTT of the digit polynomials, MAC with
-         * the GGSW, inverse NTT; CRT and accumulate */
+        /* NTT of the digit polynomials per prime */
         for (int q = 0; q < 2; q++) {
             const int64_t p = (int64_t)PR[q];
             for (size_t r = 0; r < kp1; r++) {
@@ -488,19 +516,28 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
                 nega_forward(K->NP, q, Dr);
             }
         }
-        for (size_t c = 0; c < kp1; c++) {
-            for (int q = 0; q < 2; q++) {
-                const uint64_t p = PR[q];
-                const uint64_t* Dq = D + q * kp1 * N;
-                const uint64_t* G = K->bsk_ntt[q] + (size_t)i * kp1 * kp1 * N;
-                for (int t = 0; t < N; t++) {
-                    uint64_t s = 0;
-                    for (size_t r = 0; r < kp1; r++) s = (s + Dq[r * N + t] * G[(r * kp1 + c) * N + t]) % p;
-                    res[q][t] = s;
+        for (int g = 0; g < nterms; g++) {
+            if (U == 2 && e[g] == 0) continue; /* (X^0 - 1) * y = 0 */
+            const size_t w = U == 2 ? (size_t)(i / 2) * 3 + g : (size_t)i;
+            for (size_t c = 0; c < kp1; c++) {
+                for (int q = 0; q < 2; q++) {
+                    const uint64_t p = PR[q];
+                    const uint64_t* Dq = D + q * kp1 * N;
+                    const uint64_t* G = K->bsk_ntt[q] + w * kp1 * kp1 * N;
+                    for (int t = 0; t < N; t++) {
+                        uint64_t s = 0;
+                        for (size_t r = 0; r < kp1; r++) s = (s + Dq[r * N + t] * G[(r * kp1 + c) * N + t]) % p;
+                        res[q][t] = s;
+                    }
+                    nega_inverse(K->NP, q, res[q]);
                 }
-                nega_inverse(K->NP, q, res[q]);
+                for (int t = 0; t < N; t++) Y[t] = crt2(res[0][t], res[1][t]);
+                /* acc_c += (X^e - 1) * y  (unrolled) or y (plain CMUX) */
+                for (int t = 0; t < N; t++) {
+                    uint64_t add = U == 2 ? q_sub(rot_coef(Y, N, t, (int)e[g]), Y[t]) : Y[t];
+                    acc[c * N + t] = q_add(acc[c * N + t], add);
+                }
             }
-            for (int t = 0; t < N; t++) acc[c * N + t] = q_add(acc[c * N + t], crt2(res[0][t], res[1][t]));
         }
     }
     int32_t pos[17], d[17];
@@ -521,7 +558,7 @@ void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts
         out[big] = or_conv(direct ? B[0] : apply_w(B, N, 0, nt, pos, d));
         if (direct == 2) out[big] += 1ULL << 58; /* sign gate: +-Delta/2 + Delta/2 -> {0, Delta} */
     }
-    free(acc); free(dig); free(D); free(res[0]); free(res[1]); free(V);
+    free(acc); free(dig); free(D); free(res[0]); free(res[1]); free(V); free(Y);
 }
 
 /* single LUT, rotating the LUT polynomial itself */
