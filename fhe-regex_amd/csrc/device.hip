@@ -92,6 +92,12 @@ constexpr int pad_c(int i) { return i + (i >> 4); }
 __device__ __forceinline__ uint32_t mont_lazy_d(uint32_t a, uint32_t b, uint32_t p, uint32_t pn) {
     return mont_lazy(a, b, p, pn);
 }
+// Montgomery reduction of a 64-bit sum of products T < 2^63: returns
+// T/2^32 mod p as a value below T/2^32 + p (each use states its bound).
+__device__ __forceinline__ uint32_t mont_reduce(uint64_t t, uint32_t p, uint32_t pn) {
+    const uint32_t m = (uint32_t)t * pn;
+    return (uint32_t)((t + (uint64_t)m * p) >> 32);
+}
 
 // Harvey-lazy Cooley-Tukey butterfly: x, y in [0, 4p) -> [0, 4p); w Montgomery
 __device__ __forceinline__ void ct_lazy(uint32_t& x, uint32_t& y, uint32_t w, uint32_t p, uint32_t pn) {
@@ -229,6 +235,21 @@ template <int N, int K, int E>
 constexpr int br_threads() {
     return 2 * (K + 1) * (N / E);
 }
+// FR_BR_TIMING (debug builds only, tools/build_variant.sh): wave 0 of workgroup 0
+// accumulates s_memtime deltas of the pair-step segments and prints them.
+#ifdef FR_BR_TIMING
+#define BR_STAMP(k)                                             \
+    do {                                                        \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+        tseg[k] += now_ - tlast;                                \
+        tlast = now_;                                           \
+    } while (0)
+#else
+#define BR_STAMP(k) \
+    do {            \
+    } while (0)
+#endif
+
 // bootstrapping-key unrolling factor (Params::bsk_unroll): pairs for k = 1
 template <int K>
 constexpr int br_unroll() {
@@ -421,13 +442,15 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int po = pad_c(G::template moff<LAST>(m));
-            uint32_t sacc = 0;
+            // sum_r D_r B_r in 64 bits (< 3 * 4p * p = 12p^2, and p < 0.235 * 2^32):
+            // one reduction to [0, 3.9p), one conditional subtraction to [0, 2p)
+            uint64_t ss = 0;
 #pragma unroll
             for (int r = 0; r <= K; ++r) {
                 const uint32_t d = (r == P) ? x[m] : xbuf_q_bl[2 * r * G::NP + po];
-                sacc = red2(sacc + mont_lazy_d(d, gv[r][m], pm, pn), pm);
+                ss += (uint64_t)d * gv[r][m];
             }
-            x[m] = sacc;  // [0, 2p)
+            x[m] = red2(mont_reduce(ss, pm, pn), pm);
         }
         // 4. inverse NTT and accumulate (1/N is folded into the BSK)
         inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
@@ -443,9 +466,15 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     const uint32_t* mono_q = mono + q * 2 * N;
     const uint32_t B0 = 2 * (__brev((uint32_t)bl) >> (32 - G::LOG)) + 1;  // slot bl + moff: 2 brv + 1 = B0 + c_m
     const int steps = (n + 1) / 2;
+#ifdef FR_BR_TIMING
+    uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+    const uint64_t tstart = tlast;
+#endif
     for (int t = 0; t < steps; ++t) {
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
         if ((ai | aj) == 0) continue;  // X^0*acc - acc = 0 (uniform branch)
+        BR_STAMP(0);
         // 0. prefetch the three GGSWs of this pair
         uint32_t gv[3][K + 1][E];
         {
@@ -469,8 +498,10 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             const int32_t dg = q ? rns::decompose(o, acc[m]) : rns::decompose(acc[m], o);
             x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
         }
+        BR_STAMP(1);
         // 2. forward NTT (its first exchange waits for the sibling reads above)
         forward_ntt<N, E>(x, row, zt, tl, pm, pn);
+        BR_STAMP(2);
         // 3. MAC with the three GGSWs and their monomial factors
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
@@ -485,22 +516,35 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             uint32_t d[K + 1];
 #pragma unroll
             for (int r = 0; r <= K; ++r) d[r] = (r == P) ? x[m] : xbuf_q_bl[2 * r * G::NP + po];
-            uint32_t z = 0;
+            // y_g = sum_r D_r B_gr as one 64-bit sum (d < 4p, B < p: < 8p^2; with
+            // p < 0.235 * 2^32 one reduction lands in [0, 2.9p), one subtraction of 2p
+            // in [0, 2p)); then z = sum_g y_g (psi^e_g - 1) < 6p^2, one reduction.
+            uint64_t zs = 0;
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
-                uint32_t y = 0;
+                uint64_t ys = 0;
 #pragma unroll
-                for (int r = 0; r <= K; ++r) y = red2(y + mont_lazy_d(d[r], gv[gg][r][m], pm, pn), pm);
+                for (int r = 0; r <= K; ++r) ys += (uint64_t)d[r] * gv[gg][r][m];
+                const uint32_t y = red1(mont_reduce(ys, pm, pn), 2 * pm);  // [0, 3p) -> [0, 2p)
                 const uint32_t ex = (eb[gg] + e[gg] * (uint32_t)(2 * brv_c(G::template moff<LAST>(m), G::LOG))) & (2 * N - 1);
-                z = red2(z + mont_lazy_d(y, mono_q[ex], pm, pn), pm);
+                zs += (uint64_t)y * mono_q[ex];
             }
-            x[m] = z;  // [0, 2p)
+            x[m] = red1(mont_reduce(zs, pm, pn), 2 * pm);  // [0, 3p) -> [0, 2p)
         }
+        BR_STAMP(3);
         // 4. inverse NTT and accumulate (1/N is folded into the BSK)
         inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
+        BR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) acc[m] = red1(red1(x[m], pm) + acc[m], pm);
+        BR_STAMP(5);
     }
+#ifdef FR_BR_TIMING
+    if (blockIdx.x == 0 && tid == 0)
+        printf("BR_TIMING E=%d steps=%d total=%lu decomp=%lu fwd=%lu mac=%lu inv=%lu acc=%lu top=%lu\n", E, steps,
+               (unsigned long)(__builtin_amdgcn_s_memtime() - tstart), (unsigned long)tseg[1], (unsigned long)tseg[2],
+               (unsigned long)tseg[3], (unsigned long)tseg[4], (unsigned long)tseg[5], (unsigned long)tseg[0]);
+#endif
     }
 
     // publish the accumulator: the outputs need both residues of a coefficient

@@ -45,6 +45,10 @@ constexpr uint32_t HQ0 = (uint32_t)(H_Q % P0), HQ1 = (uint32_t)(H_Q % P1);
 constexpr uint32_t DQR0 = (uint32_t)(((uint64_t)DQ0 << 32) % P0), DQR1 = (uint32_t)(((uint64_t)DQ1 << 32) % P1);
 constexpr uint32_t GENERATOR = 3;          // of both multiplicative groups
 
+// p = C * 2^K + 1 with K >= 16, so -p^-1 mod 2^32 = C * 2^K - 1 = p - 2
+constexpr uint32_t PC0 = 119, PK0 = 23, PC1 = 479, PK1 = 21;
+static_assert(P0 == PC0 * (1u << PK0) + 1 && P1 == PC1 * (1u << PK1) + 1, "prime shape");
+static_assert(PN0 == P0 - 2 && PN1 == P1 - 2, "Montgomery constant");
 FR_HD uint32_t prime(int i) { return i ? P1 : P0; }
 FR_HD uint32_t pneg(int i) { return i ? PN1 : PN0; }
 FR_HD uint64_t recip(int i) { return i ? A1 : A0; }
