@@ -240,9 +240,11 @@ constexpr int br_threads() {
 #ifdef FR_BR_TIMING
 #define BR_STAMP(k)                                             \
     do {                                                        \
+        __builtin_amdgcn_sched_barrier(0);                      \
         const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
         tseg[k] += now_ - tlast;                                \
         tlast = now_;                                           \
+        __builtin_amdgcn_sched_barrier(0);                      \
     } while (0)
 #else
 #define BR_STAMP(k) \
@@ -261,6 +263,8 @@ constexpr size_t br_smem_bytes() {
            4 * 17 * MAX_OUT + (br_unroll<K>() == 2 ? sizeof(uint32_t) * 4 * (size_t)N : 0);
 }
 constexpr int brv_c(int x, int bits) { return bits == 0 ? 0 : ((x & 1) << (bits - 1)) | brv_c(x >> 1, bits - 1); }
+// LDS position of monomial-table entry e (bank swizzle, a permutation within 32-word rows)
+__device__ __forceinline__ uint32_t mono_pos(uint32_t e) { return e ^ ((e >> 5) & 31); }
 
 // BSK NTT-domain layout [i][r][c][prime][slot]: natural (bit-reversed) slot
 // order, the same for every lane geometry E, so E can be chosen per launch.
@@ -354,7 +358,10 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             const uint32_t pq = rns::prime(qq);
             const uint32_t z = zt_all[qq * N + (int)(__brev((uint32_t)(e & (N - 1))) >> (32 - G::LOG))];
             const uint32_t v = e < N ? z : rns::negm(z, pq);
-            mono[i] = rns::subm(v, (uint32_t)((1ULL << 32) % pq), pq);  // (psi^e - 1) * 2^32 mod p
+            // (psi^e - 1) * 2^32 mod p, stored XOR-swizzled (mono_pos): within a
+            // 32-lane half the lookups are 16 e brv5(l) + c, i.e. two banks; the
+            // swizzle spreads them (22.7-way -> 1.95-way average conflict).
+            mono[qq * 2 * N + mono_pos(e)] = rns::subm(v, (uint32_t)((1ULL << 32) % pq), pq);
         }
     }
     __syncthreads();
@@ -467,7 +474,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     const uint32_t B0 = 2 * (__brev((uint32_t)bl) >> (32 - G::LOG)) + 1;  // slot bl + moff: 2 brv + 1 = B0 + c_m
     const int steps = (n + 1) / 2;
 #ifdef FR_BR_TIMING
-    uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tseg[7] = {0, 0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
     const uint64_t tstart = tlast;
 #endif
@@ -485,7 +492,11 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                 for (int r = 0; r <= K; ++r)
 #pragma unroll
                     for (int m = 0; m < E; ++m)
+#ifdef FR_BR_NOBSK  // timing experiment only: no GGSW traffic (wrong results)
+                        gv[gg][r][m] = (uint32_t)(t + gg + r + m);
+#else
                         gv[gg][r][m] = gi[(size_t)gg * ggsw + (size_t)r * (K + 1) * 2 * N + G::template moff<LAST>(m)];
+#endif
         }
         // 1. signed gadget digits of acc (the other prime's residue through LDS)
         uint32_t x[E];
@@ -506,6 +517,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
         __syncthreads();
+        BR_STAMP(6);
         const uint32_t e[3] = {(ai + aj) & (2 * N - 1), ai, aj};
         uint32_t eb[3];
 #pragma unroll
@@ -527,7 +539,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                 for (int r = 0; r <= K; ++r) ys += (uint64_t)d[r] * gv[gg][r][m];
                 const uint32_t y = red1(mont_reduce(ys, pm, pn), 2 * pm);  // [0, 3p) -> [0, 2p)
                 const uint32_t ex = (eb[gg] + e[gg] * (uint32_t)(2 * brv_c(G::template moff<LAST>(m), G::LOG))) & (2 * N - 1);
-                zs += (uint64_t)y * mono_q[ex];
+                zs += (uint64_t)y * mono_q[mono_pos(ex)];
             }
             x[m] = red1(mont_reduce(zs, pm, pn), 2 * pm);  // [0, 3p) -> [0, 2p)
         }
@@ -541,9 +553,10 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     }
 #ifdef FR_BR_TIMING
     if (blockIdx.x == 0 && tid == 0)
-        printf("BR_TIMING E=%d steps=%d total=%lu decomp=%lu fwd=%lu mac=%lu inv=%lu acc=%lu top=%lu\n", E, steps,
-               (unsigned long)(__builtin_amdgcn_s_memtime() - tstart), (unsigned long)tseg[1], (unsigned long)tseg[2],
-               (unsigned long)tseg[3], (unsigned long)tseg[4], (unsigned long)tseg[5], (unsigned long)tseg[0]);
+        printf("BR_TIMING E=%d steps=%d total=%lu decomp=%lu fwd=%lu mac_wait=%lu mac=%lu inv=%lu acc=%lu top=%lu\n", E,
+               steps, (unsigned long)(__builtin_amdgcn_s_memtime() - tstart), (unsigned long)tseg[1],
+               (unsigned long)tseg[2], (unsigned long)tseg[6], (unsigned long)tseg[3], (unsigned long)tseg[4],
+               (unsigned long)tseg[5], (unsigned long)tseg[0]);
 #endif
     }
 
