@@ -80,6 +80,7 @@ class Device {
   private:
     void ensure_arena(size_t slots);
     void ensure_batch(size_t n);
+    void ensure_digits(size_t rows);
     void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks);
     void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n);
 
@@ -90,6 +91,12 @@ class Device {
     size_t small_batch_ = 256;
     void* stream_ = nullptr;  // hipStream_t
     uint64_t* d_ksk_ = nullptr;
+    int8_t* d_kl_ = nullptr;      // KSK as balanced byte limbs [col*8 + limb][k] (MFMA keyswitch)
+    int kl_cols_ = 0;
+    bool ks_mfma_ = true;         // FR_KS_MFMA=0: the VALU lincomb+keyswitch kernel
+    int8_t* d_dig_ = nullptr;     // keyswitch digits [rows][kN*ks_level]
+    uint64_t* d_body_ = nullptr;  // lincomb'd bodies [rows]
+    size_t dig_cap_ = 0;
     uint32_t* d_bsk_ = nullptr;  // NTT domain [i][r][c][prime][slot], Montgomery form, scaled by 1/N
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
     uint64_t* d_arena_ = nullptr;

@@ -755,6 +755,94 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
     }
 }
 
+// ------------------------------------------- keyswitch on int8 MFMA
+// out[g][t] = [t == n] * body_g - sum_k D[g][k] * KSK[k][t]  (mod 2^64), with
+// D the signed base-2^3 digits of the lincomb'd mask (|d| <= 4, k = 5i + level)
+// and KSK split into 8 balanced byte limbs, KSK = sum_l L_l * 256^l (mod 2^64),
+// L_l in [-128, 128).  Each sum_k D * L_l is an exact i32 GEMM (|.| <= 4 * 128 *
+// 10240 < 2^31) on v_mfma_i32_32x32x32_i8; limbs recombine in the epilogue.
+// Layouts: D [Bp][KD] int8 (Bp = B rounded up to 32, zero rows), L [col*8 + l][KD]
+// int8 (columns padded to a multiple of 4 with zeros).
+typedef int v4i_t __attribute__((ext_vector_type(4)));
+typedef int v16i_t __attribute__((ext_vector_type(16)));
+
+// lincomb + digits: one thread per (gate, input coefficient); the body per gate
+template <int KSB, int KSL>
+__global__ void __launch_bounds__(256)
+k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride, int big,
+            int8_t* __restrict__ dig, uint64_t* __restrict__ body) {
+    const int g = blockIdx.y;
+    const DevGate& gg = gates[g];
+    const int nin = gg.n_in;
+    for (int i = blockIdx.x * 256 + threadIdx.x; i <= big; i += gridDim.x * 256) {
+        uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
+        for (int q = 0; q < nin; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i];
+        if (i == big) {
+            body[g] = v;
+        } else {
+            int32_t d[KSL];
+            ks_decompose<KSB, KSL>(v, d);
+            int8_t* o = dig + (size_t)g * big * KSL + (size_t)i * KSL;
+#pragma unroll
+            for (int j = 0; j < KSL; ++j) o[j] = (int8_t)d[j];
+        }
+    }
+}
+
+// one wave per 32 x 32 tile of (gate, limb-column); 4 waves per workgroup along
+// the column direction share the gate rows through L1
+__global__ void __launch_bounds__(256)
+k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, const uint64_t* __restrict__ body, int B,
+          int KD, int ncols /* n + 1 */, int nlc /* limb-columns, multiple of 32 */, uint64_t* __restrict__ out,
+          int out_stride) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int r = lane & 31, h = lane >> 5;
+    const int g0 = blockIdx.x * 32;
+    const int lc0 = (blockIdx.y * 4 + w) * 32;
+    if (lc0 >= nlc) return;  // whole wave
+    const int8_t* ap = dig + (size_t)(g0 + r) * KD + 16 * h;
+    const int8_t* bp = kl + (size_t)(lc0 + r) * KD + 16 * h;
+    v16i_t acc = {0};
+    for (int k = 0; k < KD; k += 32) {
+        const v4i_t a = *(const v4i_t*)(ap + k);
+        const v4i_t b = *(const v4i_t*)(bp + k);
+        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+    }
+    // lane holds D[row][lc0 + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
+    // column (lc0 + r) / 8; sum the 8 limbs of a column across lanes r^1, r^2, r^4
+    const int limb = r & 7, col = (lc0 + r) >> 3;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        uint64_t v = (uint64_t)(int64_t)acc[i] << (8 * limb);
+#pragma unroll
+        for (int s = 1; s < 8; s <<= 1) {
+            const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
+            v += ((uint64_t)hi << 32) | lo;
+        }
+        const int g = g0 + (i & 3) + 8 * (i >> 2) + 4 * h;
+        if (limb == 0 && g < B && col < ncols) out[(size_t)g * out_stride + col] = (col == ncols - 1 ? body[g] : 0) - v;
+    }
+}
+
+// KSK (u64 [k][t], t <= n) -> balanced byte limbs [t*8 + l][k]
+__global__ void __launch_bounds__(256) k_ksk_limbs(const uint64_t* __restrict__ ksk, int KD, int ncols, int nlc,
+                                                   int8_t* __restrict__ kl) {
+    const int k = blockIdx.x * 256 + threadIdx.x;
+    const int t = blockIdx.y;
+    if (k >= KD) return;
+    uint64_t x = t < ncols ? ksk[(size_t)k * ncols + t] : 0;
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        int v = (int)(x & 255);
+        x >>= 8;
+        if (v >= 128) {
+            v -= 256;
+            x += 1;
+        }
+        if (t * 8 + l < nlc) kl[(size_t)(t * 8 + l) * KD + k] = (int8_t)v;
+    }
+}
+
 // linear combination into a slot (no bootstrap): NOT of a boolean
 __global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, uint64_t* __restrict__ arena,
                                                 int slot_stride, int len) {
@@ -826,6 +914,7 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
+    if (const char* ev = std::getenv("FR_KS_MFMA")) ks_mfma_ = std::atoi(ev) != 0;
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -845,6 +934,9 @@ Device::~Device() {
     (void)hipSetDevice(dev_);
     if (stream_) (void)hipStreamSynchronize(STREAM);
     (void)hipFree(d_ksk_);
+    (void)hipFree(d_kl_);
+    (void)hipFree(d_dig_);
+    (void)hipFree(d_body_);
     (void)hipFree(d_bsk_);
     (void)hipFree(d_tw_);
     (void)hipFree(d_arena_);
@@ -877,6 +969,18 @@ void Device::ensure_arena(size_t slots) {
     }
     d_arena_ = nb;
     arena_cap_ = cap;
+}
+
+void Device::ensure_digits(size_t rows) {
+    if (rows <= dig_cap_) return;
+    size_t cap = dig_cap_ ? dig_cap_ : 1024;
+    while (cap < rows) cap *= 2;
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    (void)hipFree(d_dig_);
+    (void)hipFree(d_body_);
+    HIP_CHECK(hipMalloc(&d_dig_, cap * (size_t)p_.big() * p_.ks_level));
+    HIP_CHECK(hipMalloc(&d_body_, 8 * cap));
+    dig_cap_ = cap;
 }
 
 void Device::ensure_batch(size_t n) {
@@ -930,6 +1034,19 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
     d_bsk_ = nullptr;
     HIP_CHECK(hipMalloc(&d_ksk_, 8 * ksk.size()));
     HIP_CHECK(hipMemcpy(d_ksk_, ksk.data(), 8 * ksk.size(), hipMemcpyHostToDevice));
+    {
+        // byte-limb form of the KSK for the MFMA keyswitch
+        const int KD = p_.big() * p_.ks_level, ncols = p_.n + 1;
+        const int nlc = ((ncols * 8 + 127) / 128) * 128;  // whole 4-wave column groups
+        (void)hipFree(d_kl_);
+        d_kl_ = nullptr;
+        HIP_CHECK(hipMalloc(&d_kl_, (size_t)nlc * KD));
+        HIP_CHECK(hipMemsetAsync(d_kl_, 0, (size_t)nlc * KD, STREAM));
+        k_ksk_limbs<<<dim3((unsigned)((KD + 255) / 256), (unsigned)(nlc / 8)), 256, 0, STREAM>>>(d_ksk_, KD, ncols, nlc,
+                                                                                              d_kl_);
+        HIP_CHECK(hipGetLastError());
+        kl_cols_ = nlc;
+    }
     uint64_t* coef = nullptr;
     HIP_CHECK(hipMalloc(&coef, 8 * bsk.size()));
     HIP_CHECK(hipMemcpy(coef, bsk.data(), 8 * bsk.size(), hipMemcpyHostToDevice));
@@ -958,6 +1075,19 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
 }
 
 void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
+    if (ks_mfma_) {
+        const int KD = p_.big() * p_.ks_level;
+        const size_t bp = (n + 31) / 32 * 32;
+        ensure_digits(bp);
+        if (bp > n) HIP_CHECK(hipMemsetAsync(d_dig_ + n * KD, 0, (bp - n) * KD, STREAM));
+        k_ks_digits<3, 5><<<dim3(8, (unsigned)n), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
+                                                                     p_.big(), d_dig_, d_body_);
+        HIP_CHECK(hipGetLastError());
+        k_ks_mfma<<<dim3((unsigned)(bp / 32), (unsigned)(kl_cols_ / 128)), 256, 0, STREAM>>>(
+            d_dig_, d_kl_, d_body_, (int)n, KD, p_.n + 1, kl_cols_, d_ks, p_.ks_stride());
+        HIP_CHECK(hipGetLastError());
+        return;
+    }
     const int btiles = (int)((n + KS_BT - 1) / KS_BT);
     const int ctiles = (p_.n + 1 + KS_CT - 1) / KS_CT;
     const int chunks = (p_.big() + KS_CH - 1) / KS_CH;
