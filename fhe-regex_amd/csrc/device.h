@@ -95,7 +95,6 @@ class Device {
     int kl_cols_ = 0;
     bool ks_mfma_ = true;         // FR_KS_MFMA=0: the VALU lincomb+keyswitch kernel
     int8_t* d_dig_ = nullptr;     // keyswitch digits [rows][kN*ks_level]
-    uint64_t* d_body_ = nullptr;  // lincomb'd bodies [rows]
     size_t dig_cap_ = 0;
     uint32_t* d_bsk_ = nullptr;  // NTT domain [i][r][c][prime][slot], Montgomery form, scaled by 1/N
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]

@@ -770,7 +770,7 @@ typedef int v16i_t __attribute__((ext_vector_type(16)));
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
 k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride, int big,
-            int8_t* __restrict__ dig, uint64_t* __restrict__ body) {
+            int8_t* __restrict__ dig, uint64_t* __restrict__ body, int body_stride) {
     const int g = blockIdx.y;
     const DevGate& gg = gates[g];
     const int nin = gg.n_in;
@@ -778,7 +778,7 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
         uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
         for (int q = 0; q < nin; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i];
         if (i == big) {
-            body[g] = v;
+            body[(size_t)g * body_stride] = v;  // column n of the (zeroed) output row; the MFMA pass subtracts
         } else {
             int32_t d[KSL];
             ks_decompose<KSB, KSL>(v, d);
@@ -789,39 +789,57 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
     }
 }
 
-// one wave per 32 x 32 tile of (gate, limb-column); 4 waves per workgroup along
-// the column direction share the gate rows through L1
+// one wave per MR x 1 tiles of 32 x 32 (gate, limb-column) and one K slice
+// (blockIdx.z of gridDim.z); 4 waves per workgroup along the column direction
+// share the gate rows through L1, and the MR row tiles of a wave share each KSK
+// fragment (MR-fold less KSK traffic).  Partial results are subtracted from out
+// (pre-set to [t == n] * body) with 64-bit atomics: exact mod 2^64 in any order.
+template <int MR>
 __global__ void __launch_bounds__(256)
-k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, const uint64_t* __restrict__ body, int B,
-          int KD, int ncols /* n + 1 */, int nlc /* limb-columns, multiple of 32 */, uint64_t* __restrict__ out,
-          int out_stride) {
+k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, int KD, int ncols /* n + 1 */,
+          int nlc /* limb-columns, multiple of 32 */, unsigned long long* __restrict__ out, int out_stride) {
+    constexpr int UN = MR == 1 ? 8 : 2;  // k-steps in flight per wave
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int g0 = blockIdx.x * 32;
+    const int g0 = blockIdx.x * 32 * MR;
     const int lc0 = (blockIdx.y * 4 + w) * 32;
     if (lc0 >= nlc) return;  // whole wave
-    const int8_t* ap = dig + (size_t)(g0 + r) * KD + 16 * h;
-    const int8_t* bp = kl + (size_t)(lc0 + r) * KD + 16 * h;
-    v16i_t acc = {0};
-    for (int k = 0; k < KD; k += 32) {
-        const v4i_t a = *(const v4i_t*)(ap + k);
-        const v4i_t b = *(const v4i_t*)(bp + k);
-        acc = __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+    const int kspan = KD / gridDim.z, kb = blockIdx.z * kspan;
+    const int8_t* ap = dig + (size_t)(g0 + r) * KD + 16 * h + kb;
+    const int8_t* bp = kl + (size_t)(lc0 + r) * KD + 16 * h + kb;
+    v16i_t acc[MR];
+#pragma unroll
+    for (int t = 0; t < MR; ++t) acc[t] = v16i_t{0};
+    for (int k0 = 0; k0 < kspan; k0 += 32 * UN) {  // kspan is a multiple of 256 (host)
+        v4i_t a[UN][MR], b[UN];
+#pragma unroll
+        for (int u = 0; u < UN; ++u) {
+            b[u] = *(const v4i_t*)(bp + k0 + 32 * u);
+#pragma unroll
+            for (int t = 0; t < MR; ++t) a[u][t] = *(const v4i_t*)(ap + (size_t)t * 32 * KD + k0 + 32 * u);
+        }
+#pragma unroll
+        for (int u = 0; u < UN; ++u)
+#pragma unroll
+            for (int t = 0; t < MR; ++t) acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u][t], b[u], acc[t], 0, 0, 0);
     }
     // lane holds D[row][lc0 + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
     // column (lc0 + r) / 8; sum the 8 limbs of a column across lanes r^1, r^2, r^4
     const int limb = r & 7, col = (lc0 + r) >> 3;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        uint64_t v = (uint64_t)(int64_t)acc[i] << (8 * limb);
+    for (int t = 0; t < MR; ++t)
 #pragma unroll
-        for (int s = 1; s < 8; s <<= 1) {
-            const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
-            v += ((uint64_t)hi << 32) | lo;
+        for (int i = 0; i < 16; ++i) {
+            uint64_t v = (uint64_t)(int64_t)acc[t][i] << (8 * limb);
+#pragma unroll
+            for (int s = 1; s < 8; s <<= 1) {
+                const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
+                v += ((uint64_t)hi << 32) | lo;
+            }
+            const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (limb == 0 && g < B && col < ncols && v != 0)
+                atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
         }
-        const int g = g0 + (i & 3) + 8 * (i >> 2) + 4 * h;
-        if (limb == 0 && g < B && col < ncols) out[(size_t)g * out_stride + col] = (col == ncols - 1 ? body[g] : 0) - v;
-    }
 }
 
 // KSK (u64 [k][t], t <= n) -> balanced byte limbs [t*8 + l][k]
@@ -936,7 +954,6 @@ Device::~Device() {
     (void)hipFree(d_ksk_);
     (void)hipFree(d_kl_);
     (void)hipFree(d_dig_);
-    (void)hipFree(d_body_);
     (void)hipFree(d_bsk_);
     (void)hipFree(d_tw_);
     (void)hipFree(d_arena_);
@@ -977,9 +994,7 @@ void Device::ensure_digits(size_t rows) {
     while (cap < rows) cap *= 2;
     HIP_CHECK(hipStreamSynchronize(STREAM));
     (void)hipFree(d_dig_);
-    (void)hipFree(d_body_);
     HIP_CHECK(hipMalloc(&d_dig_, cap * (size_t)p_.big() * p_.ks_level));
-    HIP_CHECK(hipMalloc(&d_body_, 8 * cap));
     dig_cap_ = cap;
 }
 
@@ -1077,14 +1092,26 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
 void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
     if (ks_mfma_) {
         const int KD = p_.big() * p_.ks_level;
-        const size_t bp = (n + 31) / 32 * 32;
+        if (KD % 256) throw Error(FR_ERR_INVALID, "MFMA keyswitch needs kN*ks_level % 256 == 0");
+        const int MR = n >= 128 ? 4 : 1;  // row tiles per wave
+        const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
         if (bp > n) HIP_CHECK(hipMemsetAsync(d_dig_ + n * KD, 0, (bp - n) * KD, STREAM));
+        HIP_CHECK(hipMemsetAsync(d_ks, 0, (size_t)8 * p_.ks_stride() * n, STREAM));
         k_ks_digits<3, 5><<<dim3(8, (unsigned)n), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
-                                                                     p_.big(), d_dig_, d_body_);
+                                                                     p_.big(), d_dig_, d_ks + p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
-        k_ks_mfma<<<dim3((unsigned)(bp / 32), (unsigned)(kl_cols_ / 128)), 256, 0, STREAM>>>(
-            d_dig_, d_kl_, d_body_, (int)n, KD, p_.n + 1, kl_cols_, d_ks, p_.ks_stride());
+        // split K so that small batches still put ~2 waves on every SIMD
+        const int tiles = (int)(bp / (32 * MR)) * (kl_cols_ / 32);
+        int split = 1;
+        while (split < 16 && tiles * split < 2048 && (KD / 256) % (split * 2) == 0) split *= 2;
+        const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)(kl_cols_ / 128), (unsigned)split);
+        if (MR == 4)
+            k_ks_mfma<4><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                                   (unsigned long long*)d_ks, p_.ks_stride());
+        else
+            k_ks_mfma<1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                                   (unsigned long long*)d_ks, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         return;
     }
