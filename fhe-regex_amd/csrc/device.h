@@ -86,7 +86,7 @@ class Device {
 
     Params p_;
     int dev_;
-    int e_ = 16;       // residues per lane in the NTT kernels (8 or 16)
+    int e_ = 8;        // residues per lane in the NTT kernels (8 or 16; measured: 8 wins for k=1 and k=2)
     int e_small_ = 8;  // ... for launches of at most small_batch_ bootstraps
     size_t small_batch_ = 256;
     void* stream_ = nullptr;  // hipStream_t

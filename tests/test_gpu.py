@@ -59,6 +59,17 @@ def test_keyswitch_bit_exact(gctx, oracle_k1):
     assert (got == exp).all()
 
 
+@pytest.mark.parametrize("count", [1, 130, 300])
+def test_keyswitch_batch_sizes_bit_exact(gctx, oracle_k1, count):
+    """MFMA keyswitch paths: split-K single rows (1), 4-row-tile blocking with
+    padding (130 -> 256 rows), and larger batches; random (non-message) masks."""
+    rng = np.random.default_rng(count)
+    blocks = rng.integers(0, 2**64 - 1, (count, gctx.lwe_len), dtype=np.uint64, endpoint=True)
+    got = gctx.dev_keyswitch(blocks)
+    exp = oracle_k1.keyswitch(blocks)
+    assert (got == exp).all()
+
+
 def test_blind_rotate_bit_exact(gctx, oracle_k1):
     O = oracle_k1
     blocks = O.encrypt_blocks([5, 12, 0], seed=31)
