@@ -86,6 +86,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=384, help="gate bootstraps in the CPU baseline sample (0: skip)")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
     ap.add_argument("--halo", type=int, default=2, help="chars read past the last start (pattern span - 1; 2 for /abc/)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)")
     ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
     args = ap.parse_args()
 
@@ -95,11 +97,15 @@ def main():
     import torch
 
     dist = None
+    # one process per GPU; ranks beyond the visible devices (a gloo rehearsal on
+    # a one-GPU box) share devices round-robin
+    device = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(device)
+        dist.init_process_group(args.dist_backend)
+    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
 
     def barrier():
         if dist is not None:
@@ -110,7 +116,7 @@ def main():
     params = F.default_params(k=k, N=N)
     with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
         blob = f.read()
-    ctx = F.Context(local_rank, params)
+    ctx = F.Context(device, params)
     ctx.load_client_key(blob)
     t_key = time.perf_counter()
     ctx.gen_server_key(SERVER_KEY_SEED)  # same seed on every rank: identical keys, no broadcast needed
@@ -136,7 +142,7 @@ def main():
         final_pbs = 0
         if world > 1:
             lwe = ctx.download_radix(out)[0]
-            t = torch.from_numpy(lwe.view(np.int64)).cuda()
+            t = torch.from_numpy(lwe.view(np.int64)).to(coll_dev)
             parts = [torch.empty_like(t) for _ in range(world)]
             dist.all_gather(parts, t)
             if rank == 0:
@@ -186,7 +192,7 @@ def main():
 
     if dist is not None:
         tt = torch.tensor([elapsed, float(pbs_local + final_pbs_total), float(rot_local + final_pbs_total)],
-                          dtype=torch.float64, device="cuda")
+                          dtype=torch.float64, device=coll_dev)
         mx = tt.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
