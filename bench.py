@@ -82,6 +82,10 @@ def main():
     ap.add_argument("--chars", type=int, default=256, help="content chars (start offsets) per GPU")
     ap.add_argument("--pattern", default="/abc/")
     ap.add_argument("--params", default="k1n2048", choices=["k1n2048", "k2n1024"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"],
+                    help="regex evaluation: the reference's enumeration, state merging, or auto")
+    ap.add_argument("--content", default="printable", choices=["printable", "config5"],
+                    help="printable: seeded ASCII with 'abc' at 200; config5: a{3}(bc|de)*f (BASELINE config 5)")
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
     ap.add_argument("--cpu-sample", type=int, default=384, help="gate bootstraps in the CPU baseline sample (0: skip)")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
@@ -122,6 +126,7 @@ def main():
     ctx.gen_server_key(SERVER_KEY_SEED)  # same seed on every rank: identical keys, no broadcast needed
     t_key = time.perf_counter() - t_key
     ctx.set_lowering(F.LOWER_THRESHOLD if args.lowering == "threshold" else F.LOWER_FAITHFUL)
+    ctx.set_engine({"auto": F.ENGINE_AUTO, "enumerate": F.ENGINE_ENUMERATE, "merged": F.ENGINE_MERGED}[args.engine])
 
     # synthetic content: printable ASCII, "abc" planted at global position 200
     L = args.chars * world
@@ -129,6 +134,12 @@ def main():
     content = bytearray(rng.integers(0x20, 0x7F, L, dtype=np.uint8).tobytes())
     content[200:203] = b"abc"
     content = bytes(content)
+    if args.content == "config5":  # matches /^a{2,8}(bc|de)+[^xyz]$/ when L is even
+        import random
+        r5 = random.Random(5)
+        content = ("aaa" + "".join(r5.choice(["bc", "de"]) for _ in range((L - 4) // 2)) + "f").encode()
+        assert len(content) == L, "config5 content needs an even length"
+        args.halo = L  # anchored pattern: a branch reads to the end of the content
     lo, hi = F.shard_starts(L, world, rank)  # this rank's start offsets
     win_hi = min(L, hi + args.halo)          # + halo: chars a branch may read past its start
     msgs = [(c >> (2 * b)) & 3 for c in content[lo:win_hi] for b in range(4)]
@@ -250,7 +261,8 @@ def main():
         "dtype": "u64",
         "data": "synthetic: seeded printable ASCII, real encryptions under the reference fixture client key",
         "config": {"workload": f"{args.pattern} contains-match, {args.chars} chars per GPU (start-offset shards)",
-                   "content_chars": L, "params": args.params, "lowering": args.lowering,
+                   "content_chars": L, "params": args.params, "lowering": args.lowering, "engine": args.engine,
+                   "content": args.content,
                    "parallelism": f"start-offset shards x{world}"},
         "match_ms": ms_per_step,
         "blind_rotations_per_match": total_rot / args.steps,

@@ -70,6 +70,7 @@ struct fr_ctx {
     std::vector<HandleRec> handles;
     std::vector<uint32_t> free_handles;
     int lowering = FR_LOWER_THRESHOLD;
+    int engine = FR_ENGINE_AUTO;
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
 
     Device& device() {
@@ -251,7 +252,7 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
                         fr_match_stats* st) {
     double t0 = now_ms();
     ValueDag dag;
-    Recorded rec = record_has_match(dag, n, pattern ? pattern : "", lo, hi);
+    Recorded rec = record_has_match_engine(dag, n, pattern ? pattern : "", lo, hi, ctx->engine);
     Program prog = lower(dag, rec.root, ctx->lowering);
     double t1 = now_ms();
     std::vector<fr_ct> inputs(content, content + n);
@@ -379,6 +380,13 @@ int fr_set_lowering(fr_ctx* ctx, int32_t mode) {
     FR_TRY({
         NEED(ctx && (mode == FR_LOWER_FAITHFUL || mode == FR_LOWER_THRESHOLD));
         ctx->lowering = mode;
+    })
+}
+
+int fr_set_engine(fr_ctx* ctx, int32_t engine) {
+    FR_TRY({
+        NEED(ctx && engine >= FR_ENGINE_AUTO && engine <= FR_ENGINE_MERGED);
+        ctx->engine = engine;
     })
 }
 
@@ -790,12 +798,13 @@ int fr_parse(const char* pattern, char* buf, size_t len) {
     })
 }
 
-int fr_plain_match(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
-                   fr_plain_result* out) {
+int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                      int32_t engine, fr_plain_result* out) {
     FR_TRY({
         NEED((content || !len) && pattern && out && lo <= hi);
+        NEED(engine >= FR_ENGINE_AUTO && engine <= FR_ENGINE_MERGED);
         ValueDag dag;
-        Recorded rec = record_has_match(dag, len, pattern, lo, hi);
+        Recorded rec = record_has_match_engine(dag, len, pattern, lo, hi, engine);
         std::vector<int16_t> memo;
         std::memset(out, 0, sizeof *out);
         out->ct_ops = rec.ct_ops;
@@ -808,6 +817,11 @@ int fr_plain_match(const char* content, size_t len, const char* pattern, size_t 
         out->max_level_width = prog.max_width;
         out->result_lowered = eval_program(prog, (const uint8_t*)content, len);
     })
+}
+
+int fr_plain_match(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                   fr_plain_result* out) {
+    return fr_plain_match_ex(content, len, pattern, lo, hi, lowering, FR_ENGINE_ENUMERATE, out);
 }
 
 int fr_dev_keyswitch(fr_ctx* ctx, const uint64_t* in, size_t count, uint64_t* out) {

@@ -451,6 +451,13 @@ static Lazy seq_and(const Lazy& prev, const Lazy& x) {  // engine.rs:197-205
     });
 }
 
+// variants still allowed in this enumeration (record_has_match's budget)
+static thread_local size_t g_budget = SIZE_MAX;
+static void spend(size_t n) {
+    if (n > g_budget) throw Error(FR_ERR_OOM, "variant enumeration budget exceeded");
+    g_budget -= n;
+}
+
 std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
     switch (re->kind) {  // engine.rs:51-67
         case Re::SOF:
@@ -530,6 +537,7 @@ std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
                 std::vector<Branch> nxt;
                 for (auto& bp : res.back())
                     for (auto& bx : build_branches(L, re->a, bp.end)) nxt.push_back({seq_and(bp.f, bx.f), bx.end});
+                spend(nxt.size());
                 bool empty = nxt.empty();
                 res.push_back(std::move(nxt));
                 if (empty) break;
@@ -550,6 +558,7 @@ std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
                 std::vector<Branch> nxt;
                 for (auto& bp : conts)
                     for (auto& bx : build_branches(L, re->xs[i], bp.end)) nxt.push_back({seq_and(bp.f, bx.f), bx.end});
+                spend(nxt.size());
                 conts = std::move(nxt);
             }
             return conts;
@@ -559,12 +568,21 @@ std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
     throw Error(FR_ERR_REF_PANIC, "unmatched regex variant");
 }
 
-Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi) {
+Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
+                          size_t branch_budget) {
     ReP re = parse(pattern);  // engine.rs:13
     if (hi > L) hi = L;
     std::vector<Lazy> branches;
-    for (size_t i = lo; i < hi; ++i)  // engine.rs:15-18
-        for (auto& b : build_branches(L, re, i)) branches.push_back(b.f);
+    struct Budget {  // restored on every exit
+        explicit Budget(size_t b) : saved(g_budget) { g_budget = b; }
+        ~Budget() { g_budget = saved; }
+        size_t saved;
+    } budget(branch_budget);
+    for (size_t i = lo; i < hi; ++i) {  // engine.rs:15-18
+        auto bs = build_branches(L, re, i);
+        spend(bs.size());
+        for (auto& b : bs) branches.push_back(b.f);
+    }
     Execution ex(dag);
     Val res;
     if (branches.size() <= 1) {  // engine.rs:22-26
@@ -582,6 +600,20 @@ Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, s
     out.cache_hits = ex.cache_hits();
     out.n_branches = branches.size();
     return out;
+}
+
+Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
+                                 int engine) {
+    if (engine == FR_ENGINE_MERGED) return record_has_match_merged(dag, L, pattern, lo, hi);
+    if (engine == FR_ENGINE_ENUMERATE) return record_has_match(dag, L, pattern, lo, hi);
+    // AUTO: the reference's enumeration (exact counters) while it stays within
+    // a few million variants, else the state-merging evaluator
+    try {
+        return record_has_match(dag, L, pattern, lo, hi, (size_t)1 << 22);
+    } catch (const Error& e) {
+        if (e.code != FR_ERR_OOM) throw;
+    }
+    return record_has_match_merged(dag, L, pattern, lo, hi);
 }
 
 }  // namespace fr

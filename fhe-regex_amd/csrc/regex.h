@@ -99,7 +99,16 @@ struct Recorded {
     int root = -1;  // value id of the result
     uint64_t ct_ops = 0, cache_hits = 0, n_branches = 0;
 };
-// has_match, src/regex/engine.rs:8-42 (start offsets restricted to [lo, hi))
-Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi);
+// has_match, src/regex/engine.rs:8-42 (start offsets restricted to [lo, hi)).
+// branch_budget bounds the number of enumerated variants (Error FR_ERR_OOM past
+// it); the reference itself has no bound and exhausts memory instead.
+Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
+                          size_t branch_budget = SIZE_MAX);
+// State-merging evaluator (merged.cpp, beyond the reference): the same boolean,
+// polynomial in L.  Error FR_ERR_INVALID for AST shapes it does not cover.
+Recorded record_has_match_merged(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi);
+// engine: FR_ENGINE_AUTO (enumerate within a budget, else merge), _ENUMERATE, _MERGED
+Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
+                                 int engine);
 
 }  // namespace fr

@@ -32,6 +32,7 @@ HEADER = os.path.join(REPO, "include", "fheregex.h")
 FR_OK = 0
 ERR_INVALID, ERR_PARSE, ERR_REF_PANIC, ERR_NO_DEVICE, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_NON_ASCII = range(-1, -9, -1)
 LOWER_FAITHFUL, LOWER_THRESHOLD = 0, 1
+ENGINE_AUTO, ENGINE_ENUMERATE, ENGINE_MERGED = 0, 1, 2
 NULL_CT = 0xFFFFFFFF
 
 
@@ -120,6 +121,9 @@ _SIGS = {
     "fr_has_match_range": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t,
                                      C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "fr_set_engine": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_plain_match_ex": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
+                                    C.POINTER(PlainResult)]),
     "fr_plain_match": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32,
                                  C.POINTER(PlainResult)]),
     "fr_set_lowering": (C.c_int, [C.c_void_p, C.c_int32]),
@@ -183,14 +187,15 @@ def parse(pattern: str) -> str:
 
 
 def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESHOLD,
-                start_lo: int = 0, start_hi: Optional[int] = None) -> PlainResult:
+                start_lo: int = 0, start_hi: Optional[int] = None, engine: int = ENGINE_ENUMERATE) -> PlainResult:
     """Host-only symbolic run: reference counters + plaintext result of the
     recorded circuit and of the lowered PBS program."""
     if isinstance(content, str):
         content = content.encode("latin-1")
     hi = len(content) if start_hi is None else start_hi
     r = PlainResult()
-    _check(lib().fr_plain_match(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, C.byref(r)))
+    _check(lib().fr_plain_match_ex(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, engine,
+                                   C.byref(r)))
     return r
 
 
@@ -239,6 +244,11 @@ class Context:
 
     def set_lowering(self, mode: int):
         _check(lib().fr_set_lowering(self.h, mode))
+
+    def set_engine(self, engine: int):
+        """ENGINE_AUTO (default), ENGINE_ENUMERATE (the reference's variant
+        enumeration) or ENGINE_MERGED (state merging; same decrypted result)."""
+        _check(lib().fr_set_engine(self.h, engine))
 
     def set_multi_value(self, on: bool):
         _check(lib().fr_set_multi_value(self.h, int(on)))

@@ -184,6 +184,19 @@ typedef struct {
 int fr_plain_match(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                    int32_t lowering, fr_plain_result* out);
 
+/* Evaluation engine of the regex (fr_set_engine, fr_plain_match_ex):
+ * FR_ENGINE_ENUMERATE: the reference's variant enumeration (engine.rs:45-214),
+ *   exact ct_ops / cache_hits; exponential on deep variant trees (BASELINE
+ *   config 5 exhausts memory, as in the reference).
+ * FR_ENGINE_MERGED: state-merging evaluation (beyond the reference): the same
+ *   decrypted result, a circuit polynomial in the content length and of
+ *   logarithmic depth for fixed-width loops; ct_ops counts circuit operations.
+ * FR_ENGINE_AUTO (default): enumerate within 2^22 variants, else merged. */
+enum { FR_ENGINE_AUTO = 0, FR_ENGINE_ENUMERATE = 1, FR_ENGINE_MERGED = 2 };
+int fr_set_engine(fr_ctx* ctx, int32_t engine);
+int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
+                      int32_t lowering, int32_t engine, fr_plain_result* out);
+
 /* lowering modes for fr_plain_match / fr_set_lowering */
 enum { FR_LOWER_FAITHFUL = 0, FR_LOWER_THRESHOLD = 1 };
 int fr_set_lowering(fr_ctx* ctx, int32_t mode);

@@ -534,6 +534,101 @@ def has_match(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: O
     return MatchResult(res[0], ex.ct_ops, ex.cache_hits, len(branches))
 
 
+# ---------------------------------------------------------------------------
+# Position-set simulation (test oracle for the state-merging engine).  Same
+# node rules as build_branches above, evaluated on plaintext: a map from
+# content position to (OR of the branch values reaching it); presence of a key
+# = some branch structurally reaches it.  Repetitions are run per visit
+# position with the reference's exact count bounds (at_most = L - p when
+# unbounded; lo = 0 allows at_most + 1).  Pinned against has_match on fuzzed
+# patterns (tests/test_oracle.py).
+
+def _char_ok(re: Node, ch: int) -> bool:
+    k = re.kind
+    if k == "Char":
+        return ch == re.c
+    if k == "Any":
+        return True
+    if k == "Between":  # ct_ge -> smart_gt (execution.rs:93)
+        return ch > re.f and ch <= re.t
+    if k == "Range":
+        return ch in re.cs
+    if k == "Not":
+        return not _char_ok(re.a, ch)
+    raise ValueError("Not over a multi-branch operand")
+
+
+def _reach(L: int, content: bytes, re: Node, S: dict) -> dict:
+    k = re.kind
+    if k == "SOF":
+        return {0: S[0]} if 0 in S else {}
+    if k == "EOF":
+        return {L: S[L]} if L in S else {}
+    S = {p: v for p, v in S.items() if p < L}  # engine.rs:69-71
+    if not S:
+        return {}
+    out: dict = {}
+
+    def put(q, v):
+        out[q] = out.get(q, False) or v
+
+    if k in ("Char", "Any", "Between", "Range", "Not"):
+        for p, v in S.items():
+            put(p + 1, v and _char_ok(re, content[p]))
+        return out
+    if k == "Either":
+        for d in (_reach(L, content, re.a, S), _reach(L, content, re.b, S)):
+            for q, v in d.items():
+                put(q, v)
+        return out
+    if k == "Optional":
+        for q, v in _reach(L, content, re.a, S).items():
+            put(q, v)
+        for q, v in S.items():
+            put(q, v)
+        return out
+    if k == "Seq":
+        if not re.xs:
+            raise ReferencePanic("Seq{[]}: index out of bounds (engine.rs:189-190)")
+        cur = S
+        for x in re.xs:
+            cur = _reach(L, content, x, cur)
+            if not cur:
+                return {}
+        return cur
+    if k == "Repeated":
+        for p, v in S.items():
+            at_least = 0 if re.lo is None else re.lo
+            at_most = (L - p) if re.hi is None else re.hi
+            if at_least > at_most:
+                continue
+            if at_least == 0:
+                put(p, v)
+            first = max(1, at_least)
+            last = first + (at_most - at_least)
+            lev = {p: v}
+            for kk in range(1, last + 1):
+                lev = _reach(L, content, re.a, lev)
+                if not lev:
+                    break
+                if kk >= first:
+                    for q, w in lev.items():
+                        put(q, w)
+        return out
+    raise ReferencePanic("unmatched regex variant")
+
+
+def has_match_reach(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None) -> int:
+    """Plaintext result of has_match by position-set simulation (polynomial)."""
+    if isinstance(content, str):
+        content = content.encode()
+    re = parse(pattern)
+    L = len(content)
+    hi = L if start_hi is None else min(start_hi, L)
+    out = _reach(L, content, re, {p: True for p in range(start_lo, hi)})
+    return int(any(out.values()))
+
+
 if __name__ == "__main__":
     import json
     a = sys.argv[1:]

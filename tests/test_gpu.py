@@ -262,6 +262,25 @@ def test_config5_small(gctx):
         assert (st.ct_ops, st.cache_hits) == (exp.ct_ops, exp.cache_hits)
 
 
+def test_config5_512_merged(gctx):
+    """BASELINE config 5 at its full 512 chars: beyond the reference's
+    enumeration (memory), evaluated by the merged engine (AUTO falls back to it)
+    on encrypted content; results vs the oracle's position-set simulator."""
+    import random
+    pat = "/^a{2,8}(bc|de)+[^xyz]$/"
+    rng = random.Random(5)
+    c = "aaa" + "".join(rng.choice(["bc", "de"]) for _ in range(254)) + "f"
+    got, st = _config(gctx, c, pat, 11)  # engine AUTO
+    assert got == ro.has_match_reach(c, pat) == 1
+    gctx.set_engine(F.ENGINE_MERGED)
+    try:
+        bad = c[:300] + "x" + c[301:]
+        got, st = _config(gctx, bad, pat, 12)
+        assert got == ro.has_match_reach(bad, pat) == 0
+    finally:
+        gctx.set_engine(F.ENGINE_AUTO)
+
+
 def test_faithful_lowering(gctx):
     rng = np.random.default_rng(8)
     s = _printable(rng, 64)

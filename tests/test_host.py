@@ -165,3 +165,73 @@ def test_product_encrypt_matches_oracle(key_blob, oracle_k1):
     assert [ctx.decrypt_radix(a[i]) for i in range(4)] == list(b"abc~")
     with pytest.raises(ValueError):
         ctx.encrypt_str("caf\xe9", seed=1)
+
+
+# --- state-merging engine -------------------------------
+
+@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD])
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_merged_engine_golden(v, mode):
+    r = F.plain_match(v["content"], v["pattern"], mode, engine=F.ENGINE_MERGED)
+    assert (r.result_recorded, r.result_lowered) == (v["expected"], v["expected"])
+
+
+def test_merged_engine_fuzz_vs_oracle():
+    """Merged engine vs the oracle's enumerator and its position-set simulator;
+    start ranges random.  The merged engine refuses (FR_ERR_INVALID) only an
+    unbounded repetition of a nullable operand, which the reference enumerates."""
+    rng = random.Random(19)
+    n = refused = 0
+    while n < 500:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(0, 8))
+        lo = rng.randint(0, len(c))
+        hi = rng.randint(lo, len(c))
+        try:
+            exp, e_exc = ro.has_match_reach(c, p, lo, hi), None
+        except (ro.ParseError, ro.ReferencePanic) as e:
+            exp, e_exc = None, type(e).__name__
+        try:
+            r = F.plain_match(c, p, F.LOWER_THRESHOLD, start_lo=lo, start_hi=hi, engine=F.ENGINE_MERGED)
+            got, g_exc = (r.result_recorded, r.result_lowered), None
+        except (F.ParseError, F.ReferencePanic) as e:
+            got, g_exc = None, type(e).__name__
+        except F.FheRegexError as e:
+            assert e.code == -1 and "nullable" in str(e), (c, p)
+            refused += 1
+            n += 1
+            continue
+        if e_exc or g_exc:
+            assert e_exc == g_exc, (c, p, lo, hi)
+        else:
+            assert got == (exp, exp), (c, p, lo, hi)
+        n += 1
+    assert refused < n // 10
+
+
+def _config5(rng, L=512):
+    body = "".join(rng.choice(["bc", "de"]) for _ in range((L - 4) // 2))
+    return "aaa" + body + "f"
+
+
+def test_config5_merged_engine():
+    """BASELINE config 5 (/^a{2,8}(bc|de)+[^xyz]$/, 512 chars): the reference's
+    enumeration exhausts memory; AUTO falls back to the merged engine, whose
+    circuit is small and shallow, with the oracle simulator's result."""
+    rng = random.Random(5)
+    pat = "/^a{2,8}(bc|de)+[^xyz]$/"
+    c = _config5(rng)
+    assert len(c) == 512
+    flips = [c[:-1] + "x", c[:200] + "q" + c[201:], "b" + c[1:], c[:3] + "cb" + c[5:]]
+    for content in [c] + flips:
+        exp = ro.has_match_reach(content, pat)
+        r = F.plain_match(content, pat, engine=F.ENGINE_AUTO)
+        assert (r.result_recorded, r.result_lowered) == (exp, exp), content[:12]
+    assert ro.has_match_reach(c, pat) == 1 and ro.has_match_reach(flips[0], pat) == 0
+    r = F.plain_match(c, pat, engine=F.ENGINE_MERGED)
+    assert r.pbs < 20000 and r.levels <= 40, (r.pbs, r.levels)
+
+
+def test_auto_engine_keeps_reference_counts_when_enumerable():
+    a = F.plain_match("x" * 64, "/abc/", engine=F.ENGINE_AUTO)
+    assert (a.ct_ops, a.cache_hits) == (371, 0)

@@ -185,3 +185,32 @@ def test_oracle_sign_gate_fanin16(oracle_k1):
     out2 = O.gates(jobs, ones)
     dec = lambda o: [int(O.decode16(x)[0]) for x in o]
     assert dec(out0) == [0, 0] and dec(out1) == [1, 0] and dec(out2) == [1, 1]
+
+
+@pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
+def test_reach_simulator_golden(v):
+    # the position-set simulator (checker of the merged engine) on the reference's vectors
+    assert ro.has_match_reach(v["content"], v["pattern"]) == v["expected"]
+
+
+def test_reach_simulator_vs_enumerator_fuzz():
+    """Pins has_match_reach to the reference-faithful enumerator (has_match):
+    same result and same panics on fuzzed patterns/contents."""
+    import random
+
+    import regex_fuzz as rf
+    rng = random.Random(11)
+    n = 0
+    while n < 300:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(0, 7))
+        try:
+            exp, e_exc = ro.has_match(c, p).result, None
+        except (ro.ParseError, ro.ReferencePanic) as e:
+            exp, e_exc = None, type(e).__name__
+        try:
+            got, g_exc = ro.has_match_reach(c, p), None
+        except (ro.ParseError, ro.ReferencePanic) as e:
+            got, g_exc = None, type(e).__name__
+        assert (got, g_exc) == (exp, e_exc), (c, p)
+        n += 1
