@@ -51,8 +51,84 @@ using rns::red2;
 // ------------------------------------------------------------------ geometry
 constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
 
-// one padding word per 16 (conflict-free strided phases)
-__device__ __forceinline__ int lds_pad(int i) { return i + (i >> 4); }
+// LDS address maps of an exchange row (bank-conflict-free exchanges).
+//
+// A b32 LDS access of a wave is served in two 32-lane groups with bank =
+// dword address mod 32 (MI355X_MICROARCH.md §LDS).  In every phase layout the
+// lanes 0-31 of a group vary five index bits (the "group bits" of the layout),
+// so an exchange between phases p and p+1 is conflict-free iff the address map
+// sends each of the two group-bit sets to 32 distinct banks.  An additive map
+// addr(i) = sum_k w_k * bit_k(i) does that iff, within each group, the 2-adic
+// valuations of the w_k mod 32 are exactly {0..4}; no single additive map can
+// serve all four layouts of N = 2048, E = 8 (the constraints of P0/P2/P3
+// contradict), so each exchange (p, p+1) gets its own map.  Additive maps keep
+// every address one per-lane register plus a compile-time immediate.
+//
+// Construction: shared group bits and pairs (i-th private bit of each group)
+// take valuations 0, 1, ... in ascending bit order; weights are then the
+// smallest superincreasing values with those valuations (injective).  The wave
+// bits of a row (top index bits in layouts p >= 1, see wave_top) get a weight
+// CH * 2^j common to all maps, so in those layouts a wave's slots form the
+// same address chunk under every map, which is what keeps the barrier plan
+// below valid across map changes.
+struct LdsMap {
+    int w[16];
+    int span;
+};
+constexpr int geo_lo(int LOG, int e, int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
+constexpr int geo_lane_bit(int LOG, int e, int p, int b) { return b < geo_lo(LOG, e, p) ? b : b + e; }
+constexpr unsigned geo_group(int LOG, int e, int p) {
+    unsigned g = 0;
+    for (int b = 0; b < 5; ++b) g |= 1u << geo_lane_bit(LOG, e, p, b);
+    return g;
+}
+constexpr LdsMap make_lds_map(int LOG, int e, int H, int x, int nph) {
+    LdsMap m{};
+    const unsigned F = geo_group(LOG, e, x), Tg = geo_group(LOG, e, x + 1 < nph ? x + 1 : x), S = F & Tg;
+    int color[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
+    int pf[5] = {0, 0, 0, 0, 0}, pt[5] = {0, 0, 0, 0, 0};
+    int nf = 0, nt = 0;
+    for (int k = 0; k < LOG; ++k) {
+        if (((F >> k) & 1) && !((S >> k) & 1)) pf[nf++] = k;
+        if (((Tg >> k) & 1) && !((S >> k) & 1)) pt[nt++] = k;
+    }
+    int next = 0;
+    for (int k = 0; k < LOG; ++k) {
+        if (color[k] >= 0) continue;
+        if ((S >> k) & 1) {
+            color[k] = next++;
+            continue;
+        }
+        for (int i = 0; i < nf; ++i)
+            if (pf[i] == k || pt[i] == k) {
+                color[pf[i]] = color[pt[i]] = next++;
+                break;
+            }
+    }
+    int sum = 0;
+    for (int k = 0; k < H; ++k) {
+        int w = sum + 1;
+        if (color[k] >= 0)
+            while (w % (2 << color[k]) != (1 << color[k])) ++w;
+        m.w[k] = w;
+        sum += w;
+    }
+    m.span = (sum + 32) / 32 * 32;
+    return m;
+}
+struct LdsMaps {
+    LdsMap m[8];
+    int ch;
+};
+constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph) {
+    LdsMaps r{};
+    r.ch = 32;
+    for (int x = 0; x < (nph > 1 ? nph - 1 : 1); ++x) {
+        r.m[x] = make_lds_map(LOG, e, H, x, nph);
+        if (r.m[x].span > r.ch) r.ch = r.m[x].span;
+    }
+    return r;
+}
 
 // N-point negacyclic NTT spread over T = N/E lanes holding E coefficients
 // each.  The LOG = log2 N stages run as NPH register-resident phases of e =
@@ -65,16 +141,50 @@ struct NttGeo {
     static constexpr int e = ilog2c(E);
     static constexpr int T = N / E;
     static constexpr int NPH = (LOG + e - 1) / e;
-    static constexpr int NP = N + N / 16;  // padded LDS row (u32)
     static_assert((1 << LOG) == N && (1 << e) == E, "powers of two");
     static_assert(T % 64 == 0, "a (polynomial, prime) pair must own whole waves");
-    static constexpr int lo(int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
+    static constexpr int lo(int p) { return geo_lo(LOG, e, p); }
     static constexpr int s_begin(int p) { return p * e; }
     static constexpr int s_end(int p) { return (p + 1) * e < LOG ? (p + 1) * e : LOG; }
-    __device__ static __forceinline__ int pad(int i) { return lds_pad(i); }
+    // LDS address maps (above): map X serves the exchange between phases X and
+    // X+1; map 0 also serves natural-order (phase-0) accesses, map XL the
+    // last-phase (bit-reversed slot) accesses of the MAC.
+    static constexpr int WB = ilog2c(T / 64);  // wave bits of a row
+    static constexpr int H = LOG - WB;
+    static constexpr LdsMaps MAPS = make_lds_maps(LOG, e, H, NPH);
+    static constexpr int CH = MAPS.ch;
+    static constexpr int NP = CH << WB;  // LDS row (u32)
+    static constexpr int XL = NPH >= 2 ? NPH - 2 : 0;
+    // the wave bits of layout p are its top index bits [H, LOG)
+    static constexpr bool wave_top(int p) { return WB == 0 || lo(p) <= 6; }
+    template <int X>
+    static constexpr int wt(int k) {
+        return k < H ? MAPS.m[X].w[k] : CH << (k - H);
+    }
+    // address of index i under map X (constant-folds for constant i; at run
+    // time only the bits whose weight differs from 2^k cost an operation)
+    template <int X>
+    __host__ __device__ static constexpr int at(int i) {
+        int a = i;
+#pragma unroll
+        for (int k = 0; k < LOG; ++k)
+            if (wt<X>(k) != (1 << k)) a += ((i >> k) & 1) * (wt<X>(k) - (1 << k));
+        return a;
+    }
+    // conflict check: lanes 0-31 of layout p under map X hit 32 distinct banks
+    template <int X>
+    static constexpr bool banks_distinct(int p) {
+        bool seen[32] = {};
+        for (int l = 0; l < 32; ++l) {
+            const int b = at<X>(((l >> lo(p)) << (lo(p) + e)) | (l & ((1 << lo(p)) - 1))) & 31;
+            if (seen[b]) return false;
+            seen[b] = true;
+        }
+        return true;
+    }
     // element m of lane tl in phase p: idx = base(tl) | moff(m), disjoint bits,
-    // so pad(idx) = pad(base) + pad(moff) and x >> k splits the same way: every
-    // address is one per-lane register plus a compile-time immediate.
+    // so at(idx) = at(base) + at(moff): every address is one per-lane register
+    // plus a compile-time immediate.
     template <int p>
     __device__ static __forceinline__ int base(int tl) {
         constexpr int L = lo(p);
@@ -85,7 +195,6 @@ struct NttGeo {
     template <int p>
     __device__ static __forceinline__ int idx(int tl, int m) { return base<p>(tl) + moff<p>(m); }
 };
-constexpr int pad_c(int i) { return i + (i >> 4); }
 
 // Montgomery product a*b/2^32 in [0, 2p) (a*b < 4p^2).  (No inline asm in
 // this file: the waitcnt pass drains every outstanding load before one.)
@@ -100,8 +209,9 @@ __device__ __forceinline__ uint32_t mont_reduce(uint64_t t, uint32_t p, uint32_t
 }
 
 // Harvey-lazy Cooley-Tukey butterfly: x, y in [0, 4p) -> [0, 4p); w Montgomery
-__device__ __forceinline__ void ct_lazy(uint32_t& x, uint32_t& y, uint32_t w, uint32_t p, uint32_t pn) {
-    x = red2(x, p);
+// (first = true: x already in [0, 2p), the reduction is skipped)
+__device__ __forceinline__ void ct_lazy(uint32_t& x, uint32_t& y, uint32_t w, uint32_t p, uint32_t pn, bool first = false) {
+    if (!first) x = red2(x, p);
     const uint32_t t = mont_lazy_d(y, w, p, pn);  // [0, 2p)
     y = x - t + 2 * p;
     x = x + t;
@@ -126,7 +236,7 @@ __device__ __forceinline__ void fwd_phase(uint32_t (&x)[E], const uint32_t* zt, 
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             if (m & dm) continue;
-            ct_lazy(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))], pm, pn);
+            ct_lazy(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))], pm, pn, s == 0);
         }
     }
 }
@@ -172,31 +282,42 @@ __device__ __forceinline__ void wave_sync() {
 template <int N, int E, int PF, int PT, bool PRE = true>
 __device__ __forceinline__ void exchange(uint32_t (&x)[E], uint32_t* row, int tl) {
     using G = NttGeo<N, E>;
-    uint32_t* rf = row + G::pad(G::template base<PF>(tl));
-    uint32_t* rt = row + G::pad(G::template base<PT>(tl));
+    constexpr int X = PF < PT ? PF : PT;
+    uint32_t* rf = row + G::template at<X>(G::template base<PF>(tl));
+    uint32_t* rt = row + G::template at<X>(G::template base<PT>(tl));
     if constexpr (PRE) __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) rf[pad_c(G::template moff<PF>(m))] = x[m];
-    if constexpr (wave_local<N, E, PF, PT>()) wave_sync();
+    for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+    if constexpr (wave_local<N, E, PF, PT>() && G::wave_top(PF)) wave_sync();
     else __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) x[m] = rt[pad_c(G::template moff<PT>(m))];
+    for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
 }
 
 // Barrier plan (hazards between waves on the exchange rows).  After any
-// exchange every lane reads only slots its own wave owns under the new layout,
-// and those sets partition the row; so a later write to them by the same
-// wave cannot race another wave.  Only the first exchange of an NTT needs a
-// barrier before writing: the forward one follows the rotation step (other
-// waves read arbitrary slots of this row), the inverse one follows the MAC
-// (other polynomials' waves read this row).
+// exchange every lane reads only slots its own wave owns under the new layout;
+// in a wave-top layout those are the wave's own address chunk under every map,
+// so a later write of the same layout by the same wave (even under the next
+// exchange's map) cannot race another wave.  So only the first exchange of an
+// NTT needs a barrier before writing: the forward one follows the rotation
+// step (other waves read arbitrary slots of this row), the inverse one follows
+// the MAC (other polynomials' waves read this row) -- plus any exchange that
+// writes a layout that is not wave-top.
 template <int N, int E, int p>
 constexpr bool fwd_pre() {
-    return p == 0;
+    return p == 0 || !NttGeo<N, E>::wave_top(p);
 }
 template <int N, int E, int p>
 constexpr bool inv_pre() {
-    return p == NttGeo<N, E>::NPH - 1;
+    return p == NttGeo<N, E>::NPH - 1 || !NttGeo<N, E>::wave_top(p);
+}
+
+template <int N, int E, int X = 0>
+constexpr bool exchanges_conflict_free() {
+    using G = NttGeo<N, E>;
+    if constexpr (X + 1 >= G::NPH) return true;
+    else return G::template banks_distinct<X>(X) && G::template banks_distinct<X>(X + 1) &&
+                exchanges_conflict_free<N, E, X + 1>();
 }
 
 template <int N, int E, int p>
@@ -217,7 +338,7 @@ __device__ __forceinline__ void inverse_from(uint32_t (&x)[E], uint32_t* row, co
         inverse_from<N, E, p - 1>(x, row, zt, tl, pm, pn);
     }
 }
-// natural order (phase-0 layout), values < 4p -> bit-reversed slots (last-phase layout), < 4p
+// natural order (phase-0 layout), values < 2p -> bit-reversed slots (last-phase layout), < 4p
 template <int N, int E>
 __device__ __forceinline__ void forward_ntt(uint32_t (&x)[E], uint32_t* row, const uint32_t* zt, int tl, uint32_t pm,
                                             uint32_t pn) {
@@ -299,9 +420,10 @@ __device__ __forceinline__ int lut_terms(const uint8_t* lf, uint32_t* terms) {
     return nt;
 }
 // residue of sum_t d_t (X^pos_t A)[j] mod p from one residue row of A
-template <int N>
+template <class G>
 __device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint32_t* terms, int nt, int j, uint32_t pm,
                                            int q) {
+    constexpr int N = 1 << G::LOG;
     int64_t acc = 0;
     for (int t = 0; t < nt; ++t) {  // nt uniform, terms broadcast from LDS
         const uint32_t tm = terms[t];
@@ -311,7 +433,7 @@ __device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint32_t* 
             src += N;
             d = -d;
         }
-        acc += (int64_t)d * (int64_t)row[lds_pad(src)];
+        acc += (int64_t)d * (int64_t)row[G::template at<0>(src)];
     }
     // |acc| < 16 * 30 * p: shift by 512p before reducing
     return rns::reduce64((uint64_t)(acc + 512LL * pm), q);
@@ -323,6 +445,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                const uint32_t* __restrict__ bsk, const uint32_t* __restrict__ tw, uint64_t* __restrict__ arena,
                int slot_stride) {
     using G = NttGeo<N, E>;
+    static_assert(exchanges_conflict_free<N, E>(), "LDS maps must make every exchange conflict-free");
     constexpr int NT = br_threads<N, K, E>();
     constexpr int LAST = G::NPH - 1;
     extern __shared__ __attribute__((aligned(16))) uint32_t smem[];
@@ -371,11 +494,12 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     const uint32_t* row0 = xbuf + (2 * P) * G::NP;  // this polynomial, prime 0
     const uint32_t* row1 = row0 + G::NP;            // ... prime 1
     const int b0 = G::template base<0>(tl), bl = G::template base<LAST>(tl);
-    uint32_t* row_b0 = row + G::pad(b0);
-    const uint32_t* row0_b0 = row0 + G::pad(b0);
-    const uint32_t* row1_b0 = row1 + G::pad(b0);
-    uint32_t* row_bl = row + G::pad(bl);
-    const uint32_t* xbuf_q_bl = xbuf + q * G::NP + G::pad(bl);
+    constexpr int XL = G::XL;
+    uint32_t* row_b0 = row + G::template at<0>(b0);
+    const uint32_t* row0_b0 = row0 + G::template at<0>(b0);
+    const uint32_t* row1_b0 = row1 + G::template at<0>(b0);
+    uint32_t* row_bl = row + G::template at<XL>(bl);
+    const uint32_t* xbuf_q_bl = xbuf + q * G::NP + G::template at<XL>(bl);
     uint32_t acc[E];  // canonical residues, natural order: coefficient idx<0>(tl, m)
     {
         // acc = (0, X^-bbar * V): V's residues into the body rows, then rotate
@@ -389,7 +513,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                     const int mm = (jj + half) / box;
                     v = mm < 16 ? mont(lut[mm], dqr, pm, pn) : rns::negm(mont(lut[0], dqr, pm, pn), pm);
                 }
-                row[G::pad(jj)] = v;
+                row[G::template at<0>(jj)] = v;
             }
         }
         __syncthreads();
@@ -397,7 +521,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int s = (b0 + G::template moff<0>(m) + (int)bbar) & (2 * N - 1);
-            const uint32_t v = row[G::pad(s & (N - 1))];
+            const uint32_t v = row[G::template at<0>(s & (N - 1))];
             acc[m] = body ? (s < N ? v : rns::negm(v, pm)) : 0u;
         }
         __syncthreads();  // the rotated reads above touch slots other waves write next
@@ -423,19 +547,19 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         // (no barrier before the write: the last inverse exchange left these
         // slots read by this wave only)
 #pragma unroll
-        for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
+        for (int m = 0; m < E; ++m) row_b0[G::template at<0>(G::template moff<0>(m))] = acc[m];
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int j = b0 + G::template moff<0>(m);
             const int s = (j - a) & (2 * N - 1);
-            const int sp = G::pad(s < N ? s : s - N);
+            const int sp = G::template at<0>(s < N ? s : s - N);
             uint32_t v0 = row0[sp], v1 = row1[sp];
             if (s >= N) {
                 v0 = rns::negm(v0, rns::P0);
                 v1 = rns::negm(v1, rns::P1);
             }
-            const int jo = pad_c(G::template moff<0>(m));
+            const int jo = G::template at<0>(G::template moff<0>(m));
             const int32_t dg = rns::decompose(rns::subm(v0, row0_b0[jo], rns::P0), rns::subm(v1, row1_b0[jo], rns::P1));
             x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
         }
@@ -444,11 +568,11 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         // 3. external product MAC (in place): x_(P,q) = sum_r D_(r,q) * GGSW_i[r][P][q]
         //    (no barrier before the write: these slots were last read by this wave)
 #pragma unroll
-        for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
+        for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const int po = pad_c(G::template moff<LAST>(m));
+            const int po = G::template at<XL>(G::template moff<LAST>(m));
             // sum_r D_r B_r in 64 bits (< 3 * 4p * p = 12p^2, and p < 0.235 * 2^32):
             // one reduction to [0, 3.9p), one conditional subtraction to [0, 2p)
             uint64_t ss = 0;
@@ -469,7 +593,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     //   acc += sum_g (X^e_g - 1) * (GGSW_3t+g [x] acc),  e = (a_i + a_j, a_i, a_j),
     // with one decomposition of acc, one forward NTT per polynomial, the three
     // monomial factors applied slot-wise in the NTT domain, one inverse NTT.
-    const uint32_t* sib_b0 = xbuf + (2 * P + (1 - q)) * G::NP + G::pad(b0);  // other prime, same polynomial
+    const uint32_t* sib_b0 = xbuf + (2 * P + (1 - q)) * G::NP + G::template at<0>(b0);  // other prime, same polynomial
     const uint32_t* mono_q = mono + q * 2 * N;
     const uint32_t B0 = 2 * (__brev((uint32_t)bl) >> (32 - G::LOG)) + 1;  // slot bl + moff: 2 brv + 1 = B0 + c_m
     const int steps = (n + 1) / 2;
@@ -501,11 +625,11 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         // 1. signed gadget digits of acc (the other prime's residue through LDS)
         uint32_t x[E];
 #pragma unroll
-        for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
+        for (int m = 0; m < E; ++m) row_b0[G::template at<0>(G::template moff<0>(m))] = acc[m];
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const uint32_t o = sib_b0[pad_c(G::template moff<0>(m))];
+            const uint32_t o = sib_b0[G::template at<0>(G::template moff<0>(m))];
             const int32_t dg = q ? rns::decompose(o, acc[m]) : rns::decompose(acc[m], o);
             x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
         }
@@ -515,7 +639,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         BR_STAMP(2);
         // 3. MAC with the three GGSWs and their monomial factors
 #pragma unroll
-        for (int m = 0; m < E; ++m) row_bl[pad_c(G::template moff<LAST>(m))] = x[m];
+        for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
         __syncthreads();
         BR_STAMP(6);
         const uint32_t e[3] = {(ai + aj) & (2 * N - 1), ai, aj};
@@ -524,20 +648,21 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
         for (int gg = 0; gg < 3; ++gg) eb[gg] = __builtin_amdgcn_readfirstlane(e[gg]) * B0;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const int po = pad_c(G::template moff<LAST>(m));
+            const int po = G::template at<XL>(G::template moff<LAST>(m));
             uint32_t d[K + 1];
 #pragma unroll
             for (int r = 0; r <= K; ++r) d[r] = (r == P) ? x[m] : xbuf_q_bl[2 * r * G::NP + po];
             // y_g = sum_r D_r B_gr as one 64-bit sum (d < 4p, B < p: < 8p^2; with
-            // p < 0.235 * 2^32 one reduction lands in [0, 2.9p), one subtraction of 2p
-            // in [0, 2p)); then z = sum_g y_g (psi^e_g - 1) < 6p^2, one reduction.
+            // p < 0.235 * 2^32 one reduction lands in [0, 2.87p)); then
+            // z = sum_g y_g (psi^e_g - 1) < 8.6p^2 < 2^63, one reduction to
+            // [0, 3p) and one subtraction of 2p: [0, 2p).
             uint64_t zs = 0;
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
                 uint64_t ys = 0;
 #pragma unroll
                 for (int r = 0; r <= K; ++r) ys += (uint64_t)d[r] * gv[gg][r][m];
-                const uint32_t y = red1(mont_reduce(ys, pm, pn), 2 * pm);  // [0, 3p) -> [0, 2p)
+                const uint32_t y = mont_reduce(ys, pm, pn);  // [0, 2.87p)
                 const uint32_t ex = (eb[gg] + e[gg] * (uint32_t)(2 * brv_c(G::template moff<LAST>(m), G::LOG))) & (2 * N - 1);
                 zs += (uint64_t)y * mono_q[mono_pos(ex)];
             }
@@ -563,7 +688,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
     // publish the accumulator: the outputs need both residues of a coefficient
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) row_b0[pad_c(G::template moff<0>(m))] = acc[m];
+    for (int m = 0; m < E; ++m) row_b0[G::template at<0>(G::template moff<0>(m))] = acc[m];
     __syncthreads();
     const int big = K * N;
     if (kind != JOB_MULTI) {
@@ -575,7 +700,8 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
             const int j = t == 0 ? 0 : N - t;
             const uint32_t* r0 = xbuf + 2 * pp * G::NP;
-            uint32_t v0 = r0[G::pad(j)], v1 = r0[G::NP + G::pad(j)];
+            const int aj = G::template at<0>(j);
+            uint32_t v0 = r0[aj], v1 = r0[G::NP + aj];
             if (t != 0) {
                 v0 = rns::negm(v0, rns::P0);
                 v1 = rns::negm(v1, rns::P1);
@@ -595,7 +721,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
             const int j = t == 0 ? 0 : N - t;
             const uint32_t* r0 = xbuf + 2 * pp * G::NP;
-            uint32_t v0 = w_step<N>(r0, tf, nt, j, rns::P0, 0), v1 = w_step<N>(r0 + G::NP, tf, nt, j, rns::P1, 1);
+            uint32_t v0 = w_step<G>(r0, tf, nt, j, rns::P0, 0), v1 = w_step<G>(r0 + G::NP, tf, nt, j, rns::P1, 1);
             if (t != 0) {
                 v0 = rns::negm(v0, rns::P0);
                 v1 = rns::negm(v1, rns::P1);
@@ -657,23 +783,23 @@ k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const
     forward_ntt<N, E>(x, row, zt, tl, pm, pn);
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<LAST>(tl, m))] = x[m];
+    for (int m = 0; m < E; ++m) row[G::template at<G::XL>(G::template idx<LAST>(tl, m))] = x[m];
     __syncthreads();
     // a*b/R, then * R^2/N / R
     const uint32_t r2n = q ? r2n1 : r2n0;
 #pragma unroll
     for (int m = 0; m < E; ++m) {
-        const int pos = G::pad(G::template idx<LAST>(tl, m));
+        const int pos = G::template at<G::XL>(G::template idx<LAST>(tl, m));
         const uint32_t u = red1(red2(xbuf[q * G::NP + pos], pm), pm);  // operand a, canonical
         x[m] = mont(mont_lazy(u, xbuf[(2 + q) * G::NP + pos], pm, pn), r2n, pm, pn);
     }
     inverse_ntt<N, E>(x, row, zt, tl, pm, pn);
     __syncthreads();
 #pragma unroll
-    for (int m = 0; m < E; ++m) row[G::pad(G::template idx<0>(tl, m))] = red1(x[m], pm);
+    for (int m = 0; m < E; ++m) row[G::template at<0>(G::template idx<0>(tl, m))] = red1(x[m], pm);
     __syncthreads();
     for (int c = tid; c < N; c += 4 * G::T)
-        out[(size_t)blockIdx.x * N + c] = rns::crt(xbuf[G::pad(c)], xbuf[G::NP + G::pad(c)]);
+        out[(size_t)blockIdx.x * N + c] = rns::crt(xbuf[G::template at<0>(c)], xbuf[G::NP + G::template at<0>(c)]);
 }
 
 // ------------------------------------------------- lincomb + keyswitch

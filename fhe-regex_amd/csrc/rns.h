@@ -100,7 +100,8 @@ FR_HD uint64_t crt(uint32_t r0, uint32_t r1) { return (uint64_t)r0 + (uint64_t)P
 // (k * DIG_M + 2^37) >> 38 in [0, 2^23], recentred to [-2^22, 2^22).
 // (x - digit * G) mod Q stays within 0.51 G.
 constexpr uint32_t DIG_M = 2295431371u;  // round(2^61 / p1)
-FR_HD uint32_t crt_k(uint32_t r0, uint32_t r1) { return mont(subm(r1, r0, P1), CRT_CR, P1, PN1); }
+// (r1 - r0 + p1 in (0, 2p1): mont_lazy takes it unreduced)
+FR_HD uint32_t crt_k(uint32_t r0, uint32_t r1) { return mont(r1 - r0 + P1, CRT_CR, P1, PN1); }
 FR_HD int32_t digit_of_k(uint32_t k) {
     const uint32_t t = (uint32_t)(((uint64_t)k * DIG_M + (1ULL << 37)) >> 38);
     return t >= (1u << 22) ? (int32_t)t - (1 << 23) : (int32_t)t;
