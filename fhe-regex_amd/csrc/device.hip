@@ -439,6 +439,39 @@ __device__ __forceinline__ uint32_t w_step(const uint32_t* row, const uint32_t* 
     return rns::reduce64((uint64_t)(acc + 512LL * pm), q);
 }
 
+// Signed gadget digits of the accumulator, split between the two prime lanes
+// of each coefficient: the prime-Q lane decomposes elements [Q*E/2, (Q+1)*E/2)
+// from both residues, so each digit is computed once.  Round 1 hands the
+// sibling the residues it needs, round 2 the digits it did not compute (both in
+// this lane's own row, at disjoint slots).  The caller's next write of the row
+// (the forward NTT's first exchange) is preceded by a barrier.
+#ifndef FR_SPLIT_DIGITS
+#define FR_SPLIT_DIGITS 1
+#endif
+template <int N, int E, int Q>
+__device__ __forceinline__ void split_digits(uint32_t (&x)[E], const uint32_t (&acc)[E], uint32_t* row_b0,
+                                             const uint32_t* sib_b0, uint32_t pm) {
+    using G = NttGeo<N, E>;
+    constexpr int HE = E / 2, M0 = Q * HE, O0 = (1 - Q) * HE;
+#pragma unroll
+    for (int h = 0; h < HE; ++h) row_b0[G::template at<0>(G::template moff<0>(O0 + h))] = acc[O0 + h];
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < HE; ++h) {
+        const int off = G::template at<0>(G::template moff<0>(M0 + h));
+        const uint32_t o = sib_b0[off];
+        const int32_t dg = Q ? rns::decompose(o, acc[M0 + h]) : rns::decompose(acc[M0 + h], o);
+        row_b0[off] = (uint32_t)dg;
+        x[M0 + h] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < HE; ++h) {
+        const int32_t dg = (int32_t)sib_b0[G::template at<0>(G::template moff<0>(O0 + h))];
+        x[O0 + h] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
+    }
+}
+
 template <int N, int K, int E>
 __global__ void __launch_bounds__(2 * (K + 1) * (N / E), br_min_waves<E>())
 k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
@@ -622,8 +655,13 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
                         gv[gg][r][m] = gi[(size_t)gg * ggsw + (size_t)r * (K + 1) * 2 * N + G::template moff<LAST>(m)];
 #endif
         }
-        // 1. signed gadget digits of acc (the other prime's residue through LDS)
+        // 1. signed gadget digits of acc, split between the two prime lanes of a
+        //    coefficient (residues and digits swapped through LDS)
         uint32_t x[E];
+#if FR_SPLIT_DIGITS
+        if (q == 0) split_digits<N, E, 0>(x, acc, row_b0, sib_b0, pm);
+        else split_digits<N, E, 1>(x, acc, row_b0, sib_b0, pm);
+#else
 #pragma unroll
         for (int m = 0; m < E; ++m) row_b0[G::template at<0>(G::template moff<0>(m))] = acc[m];
         __syncthreads();
@@ -633,6 +671,7 @@ k_blind_rotate(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevG
             const int32_t dg = q ? rns::decompose(o, acc[m]) : rns::decompose(acc[m], o);
             x[m] = dg >= 0 ? (uint32_t)dg : (uint32_t)(dg + (int32_t)pm);
         }
+#endif
         BR_STAMP(1);
         // 2. forward NTT (its first exchange waits for the sibling reads above)
         forward_ntt<N, E>(x, row, zt, tl, pm, pn);
