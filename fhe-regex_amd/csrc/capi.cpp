@@ -29,6 +29,7 @@ Params params_from_c(const fr_params* c) {
         p.ks_level = c->ks_level;
         p.pbs_base_log = c->pbs_base_log;
         p.pbs_level = c->pbs_level;
+        p.ring = c->ring;
         p.lwe_sigma = c->lwe_sigma;
         p.glwe_sigma = c->glwe_sigma;
     }
@@ -40,6 +41,8 @@ void validate_params(const Params& p) {
         throw Error(FR_ERR_INVALID, "invalid params");
     if (p.pbs_base_log != 23 || p.pbs_level != 1) throw Error(FR_ERR_INVALID, "only the 2^23 x 1 PBS gadget is supported");
     if (p.ks_base_log < 1 || p.ks_base_log * p.ks_level > 63) throw Error(FR_ERR_INVALID, "invalid keyswitch gadget");
+    if (p.ring != FR_RING_RNS && p.ring != FR_RING_FFT) throw Error(FR_ERR_INVALID, "invalid ring");
+    if (p.ring == FR_RING_FFT && p.k != 1) throw Error(FR_ERR_INVALID, "the FFT ring is built for k = 1");
 }
 
 struct Block {
@@ -356,6 +359,7 @@ int fr_default_params(fr_params* out) {
         out->ks_level = p.ks_level;
         out->pbs_base_log = p.pbs_base_log;
         out->pbs_level = p.pbs_level;
+        out->ring = p.ring;
         out->lwe_sigma = p.lwe_sigma;
         out->glwe_sigma = p.glwe_sigma;
     })

@@ -48,7 +48,7 @@ class Device {
 
     // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod Q [i][r][c][coef]
     void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
-    bool has_keys() const { return d_ksk_ && d_bsk_; }
+    bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk_); }
 
     // arena of big-LWE slots
     int alloc_slot();
@@ -83,6 +83,11 @@ class Device {
     void ensure_digits(size_t rows);
     void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks);
     void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n);
+    // FR_RING_FFT (fft.hip)
+    void init_fft();
+    void upload_fft_bsk(const std::vector<uint64_t>& bsk);
+    void launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream);
+    void free_fft();
 
     Params p_;
     int dev_;
@@ -98,6 +103,13 @@ class Device {
     size_t dig_cap_ = 0;
     uint32_t* d_bsk_ = nullptr;  // NTT domain [i][r][c][prime][slot], Montgomery form, scaled by 1/N
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
+    // FR_RING_FFT: Fourier BSK [w][r][c][m][lane] (complex f64, scaled by 1/M), twiddles,
+    // psi quadrant table, leaf exponents (fft.h)
+    int fft_e_ = 8;
+    double* d_fbsk_ = nullptr;
+    double* d_ftw_ = nullptr;
+    double* d_fqt_ = nullptr;
+    uint16_t* d_fleaf_ = nullptr;
     uint64_t* d_arena_ = nullptr;
     size_t arena_cap_ = 0;
     std::vector<int> free_slots_;

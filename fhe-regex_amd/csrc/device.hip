@@ -30,6 +30,7 @@
 #include <type_traits>
 
 #include "device.h"
+#include "geo.h"  // lane geometry and conflict-free LDS maps (shared with fft.hip)
 #include "keys.h"
 #include "rns.h"
 
@@ -47,154 +48,6 @@ using rns::mont;
 using rns::mont_lazy;
 using rns::red1;
 using rns::red2;
-
-// ------------------------------------------------------------------ geometry
-constexpr int ilog2c(int x) { return x <= 1 ? 0 : 1 + ilog2c(x / 2); }
-
-// LDS address maps of an exchange row (bank-conflict-free exchanges).
-//
-// A b32 LDS access of a wave is served in two 32-lane groups with bank =
-// dword address mod 32 (MI355X_MICROARCH.md §LDS).  In every phase layout the
-// lanes 0-31 of a group vary five index bits (the "group bits" of the layout),
-// so an exchange between phases p and p+1 is conflict-free iff the address map
-// sends each of the two group-bit sets to 32 distinct banks.  An additive map
-// addr(i) = sum_k w_k * bit_k(i) does that iff, within each group, the 2-adic
-// valuations of the w_k mod 32 are exactly {0..4}; no single additive map can
-// serve all four layouts of N = 2048, E = 8 (the constraints of P0/P2/P3
-// contradict), so each exchange (p, p+1) gets its own map.  Additive maps keep
-// every address one per-lane register plus a compile-time immediate.
-//
-// Construction: shared group bits and pairs (i-th private bit of each group)
-// take valuations 0, 1, ... in ascending bit order; weights are then the
-// smallest superincreasing values with those valuations (injective).  The wave
-// bits of a row (top index bits in layouts p >= 1, see wave_top) get a weight
-// CH * 2^j common to all maps, so in those layouts a wave's slots form the
-// same address chunk under every map, which is what keeps the barrier plan
-// below valid across map changes.
-struct LdsMap {
-    int w[16];
-    int span;
-};
-constexpr int geo_lo(int LOG, int e, int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
-constexpr int geo_lane_bit(int LOG, int e, int p, int b) { return b < geo_lo(LOG, e, p) ? b : b + e; }
-constexpr unsigned geo_group(int LOG, int e, int p) {
-    unsigned g = 0;
-    for (int b = 0; b < 5; ++b) g |= 1u << geo_lane_bit(LOG, e, p, b);
-    return g;
-}
-constexpr LdsMap make_lds_map(int LOG, int e, int H, int x, int nph) {
-    LdsMap m{};
-    const unsigned F = geo_group(LOG, e, x), Tg = geo_group(LOG, e, x + 1 < nph ? x + 1 : x), S = F & Tg;
-    int color[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
-    int pf[5] = {0, 0, 0, 0, 0}, pt[5] = {0, 0, 0, 0, 0};
-    int nf = 0, nt = 0;
-    for (int k = 0; k < LOG; ++k) {
-        if (((F >> k) & 1) && !((S >> k) & 1)) pf[nf++] = k;
-        if (((Tg >> k) & 1) && !((S >> k) & 1)) pt[nt++] = k;
-    }
-    int next = 0;
-    for (int k = 0; k < LOG; ++k) {
-        if (color[k] >= 0) continue;
-        if ((S >> k) & 1) {
-            color[k] = next++;
-            continue;
-        }
-        for (int i = 0; i < nf; ++i)
-            if (pf[i] == k || pt[i] == k) {
-                color[pf[i]] = color[pt[i]] = next++;
-                break;
-            }
-    }
-    int sum = 0;
-    for (int k = 0; k < H; ++k) {
-        int w = sum + 1;
-        if (color[k] >= 0)
-            while (w % (2 << color[k]) != (1 << color[k])) ++w;
-        m.w[k] = w;
-        sum += w;
-    }
-    m.span = (sum + 32) / 32 * 32;
-    return m;
-}
-struct LdsMaps {
-    LdsMap m[8];
-    int ch;
-};
-constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph) {
-    LdsMaps r{};
-    r.ch = 32;
-    for (int x = 0; x < (nph > 1 ? nph - 1 : 1); ++x) {
-        r.m[x] = make_lds_map(LOG, e, H, x, nph);
-        if (r.m[x].span > r.ch) r.ch = r.m[x].span;
-    }
-    return r;
-}
-
-// N-point negacyclic NTT spread over T = N/E lanes holding E coefficients
-// each.  The LOG = log2 N stages run as NPH register-resident phases of e =
-// log2 E stages; phase p's lane owns the E elements that differ in index bits
-// [lo(p), lo(p)+e), and two consecutive phases are joined by one LDS
-// exchange.  Forward stage s pairs bit LOG-1-s with zeta[(1<<s) + (j >> (LOG-s))].
-template <int N, int E>
-struct NttGeo {
-    static constexpr int LOG = ilog2c(N);
-    static constexpr int e = ilog2c(E);
-    static constexpr int T = N / E;
-    static constexpr int NPH = (LOG + e - 1) / e;
-    static_assert((1 << LOG) == N && (1 << e) == E, "powers of two");
-    static_assert(T % 64 == 0, "a (polynomial, prime) pair must own whole waves");
-    static constexpr int lo(int p) { return geo_lo(LOG, e, p); }
-    static constexpr int s_begin(int p) { return p * e; }
-    static constexpr int s_end(int p) { return (p + 1) * e < LOG ? (p + 1) * e : LOG; }
-    // LDS address maps (above): map X serves the exchange between phases X and
-    // X+1; map 0 also serves natural-order (phase-0) accesses, map XL the
-    // last-phase (bit-reversed slot) accesses of the MAC.
-    static constexpr int WB = ilog2c(T / 64);  // wave bits of a row
-    static constexpr int H = LOG - WB;
-    static constexpr LdsMaps MAPS = make_lds_maps(LOG, e, H, NPH);
-    static constexpr int CH = MAPS.ch;
-    static constexpr int NP = CH << WB;  // LDS row (u32)
-    static constexpr int XL = NPH >= 2 ? NPH - 2 : 0;
-    // the wave bits of layout p are its top index bits [H, LOG)
-    static constexpr bool wave_top(int p) { return WB == 0 || lo(p) <= 6; }
-    template <int X>
-    static constexpr int wt(int k) {
-        return k < H ? MAPS.m[X].w[k] : CH << (k - H);
-    }
-    // address of index i under map X (constant-folds for constant i; at run
-    // time only the bits whose weight differs from 2^k cost an operation)
-    template <int X>
-    __host__ __device__ static constexpr int at(int i) {
-        int a = i;
-#pragma unroll
-        for (int k = 0; k < LOG; ++k)
-            if (wt<X>(k) != (1 << k)) a += ((i >> k) & 1) * (wt<X>(k) - (1 << k));
-        return a;
-    }
-    // conflict check: lanes 0-31 of layout p under map X hit 32 distinct banks
-    template <int X>
-    static constexpr bool banks_distinct(int p) {
-        bool seen[32] = {};
-        for (int l = 0; l < 32; ++l) {
-            const int b = at<X>(((l >> lo(p)) << (lo(p) + e)) | (l & ((1 << lo(p)) - 1))) & 31;
-            if (seen[b]) return false;
-            seen[b] = true;
-        }
-        return true;
-    }
-    // element m of lane tl in phase p: idx = base(tl) | moff(m), disjoint bits,
-    // so at(idx) = at(base) + at(moff): every address is one per-lane register
-    // plus a compile-time immediate.
-    template <int p>
-    __device__ static __forceinline__ int base(int tl) {
-        constexpr int L = lo(p);
-        return ((tl >> L) << (L + e)) | (tl & ((1 << L) - 1));
-    }
-    template <int p>
-    static constexpr int moff(int m) { return m << lo(p); }
-    template <int p>
-    __device__ static __forceinline__ int idx(int tl, int m) { return base<p>(tl) + moff<p>(m); }
-};
 
 // Montgomery product a*b/2^32 in [0, 2p) (a*b < 4p^2).  (No inline asm in
 // this file: the waitcnt pass drains every outstanding load before one.)
@@ -1050,6 +903,7 @@ static void set_smem_attr() {
 }
 
 static bool supported(const Params& p) {
+    if (p.ring == FR_RING_FFT) return p.N == 2048 && p.k == 1;
     return (p.N == 2048 && p.k == 1) || (p.N == 1024 && p.k == 2) || (p.N == 1024 && p.k == 1);
 }
 
@@ -1109,6 +963,7 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         for (int i = 0; i < p.N; ++i) tw[(size_t)q * p.N + i] = (uint32_t)(((uint64_t)T.zeta[q][i] << 32) % rns::prime(q));
     HIP_CHECK(hipMalloc(&d_tw_, 4 * tw.size()));
     HIP_CHECK(hipMemcpy(d_tw_, tw.data(), 4 * tw.size(), hipMemcpyHostToDevice));
+    if (p.ring == FR_RING_FFT) init_fft();
     ensure_arena(1024);
     ensure_batch(1024);
 }
@@ -1121,6 +976,7 @@ Device::~Device() {
     (void)hipFree(d_dig_);
     (void)hipFree(d_bsk_);
     (void)hipFree(d_tw_);
+    free_fft();
     (void)hipFree(d_arena_);
     (void)hipFree(d_gates_);
     (void)hipFree(d_ks_);
@@ -1134,7 +990,9 @@ std::string Device::info() const {
     hipDeviceProp_t prop;
     (void)hipGetDeviceProperties(&prop, dev_);
     std::ostringstream o;
-    o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount << " E=" << e_;
+    o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount;
+    if (p_.ring == FR_RING_FFT) o << " ring=fft E=" << fft_e_;
+    else o << " ring=rns E=" << e_;
     return o.str();
 }
 
@@ -1227,6 +1085,10 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
         HIP_CHECK(hipGetLastError());
         kl_cols_ = nlc;
     }
+    if (p_.ring == FR_RING_FFT) {
+        upload_fft_bsk(bsk);
+        return;
+    }
     uint64_t* coef = nullptr;
     HIP_CHECK(hipMalloc(&coef, 8 * bsk.size()));
     HIP_CHECK(hipMemcpy(coef, bsk.data(), 8 * bsk.size(), hipMemcpyHostToDevice));
@@ -1296,6 +1158,10 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
 }
 
 void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
+    if (p_.ring == FR_RING_FFT) {
+        launch_br_fft(d_gates, d_ks, n, stream_);
+        return;
+    }
     // small levels (at most one bootstrap per CU): more lanes per bootstrap for latency
     const int E = n <= small_batch_ ? e_small_ : e_;
     dispatch(p_, E, [&](auto n_, auto k_, auto e_c) {
@@ -1436,6 +1302,7 @@ int lut_w_norm2(const uint8_t* lut) {
 }
 
 void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, uint64_t* out) {
+    if (p_.ring != FR_RING_RNS) throw Error(FR_ERR_INVALID, "ring_mul test hook: RNS ring only");
     const int N = p_.N;
     uint64_t *da, *db, *dout;
     HIP_CHECK(hipMalloc(&da, 8 * count * N));

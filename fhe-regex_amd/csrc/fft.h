@@ -1,0 +1,133 @@
+// The torus ring of the blind rotation: T_64[X]/(X^N+1) (coefficients mod
+// 2^64, as in tfhe-rs), polynomial products through an f64 negacyclic FFT —
+// the same representation tfhe-rs 0.2 uses for its Fourier bootstrapping key
+// (reference Cargo.lock:602-615, concrete-fft 0.1.0 at Cargo.lock:110-114).
+//
+// Transform: a real polynomial a of degree < N folds into M = N/2 complex
+// points z_k = a_k + i a_(k+M), i.e. a mod (x^M - i) with x^M = i.  The M roots
+// of x^M - i are psi^L (psi = e^(i pi / N), L = 1 mod 4); the forward
+// transform is the merged-twiddle Cooley-Tukey split of x^M - i:
+//   node (s, b) holds z mod (x^(M/2^s) - psi^E(s,b)),  E(0,0) = M,
+//   children E/2 and E/2 + N (mod 2N), butterfly twiddle c = psi^(E/2):
+//       (lo, hi) -> (lo + c hi, lo - c hi)                       (forward)
+//       (A, B)   -> (A + B, conj(c) (A - B))   (inverse, times 2 per stage)
+// so after log2 M stages slot j holds a(psi^L(j)) with L(j) = E(log2 M, j).
+// The inverse therefore returns M * z; the 1/M = 2^-log2(M) factor (exact in
+// f64) is folded into the Fourier bootstrapping key.  Multiplying by X^e is
+// the slot-wise factor psi^(e L(j) mod 2N).
+//
+// Every floating-point step is a fixed sequence of IEEE-754 double operations
+// (mul, add, fma; -ffp-contract=off everywhere), so the device kernel, the
+// host key transform and oracle/tfhe_oracle.c's restatement agree bit for bit.
+// Twiddles are computed once on the host (psi_pow) and uploaded.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <vector>
+
+#include "common.h"
+
+namespace fr {
+namespace fft {
+
+struct c64 {
+    double re, im;
+};
+
+#if defined(__HIPCC__)
+#define FR_FMA(a, b, c) __builtin_fma((a), (b), (c))
+#else
+#define FR_FMA(a, b, c) std::fma((a), (b), (c))
+#endif
+
+// a * b: re = fma(a.re, b.re, -(a.im b.im)), im = fma(a.re, b.im, a.im b.re)
+FR_HD void cmul(double ar, double ai, double br, double bi, double& zr, double& zi) {
+    const double pr = -(ai * bi), pi = ai * br;
+    zr = FR_FMA(ar, br, pr);
+    zi = FR_FMA(ar, bi, pi);
+}
+// z += a * b: re = fma(-a.im, b.im, fma(a.re, b.re, z.re)), im = fma(a.im, b.re, fma(a.re, b.im, z.im))
+FR_HD void cmac(double ar, double ai, double br, double bi, double& zr, double& zi) {
+    zr = FR_FMA(-ai, bi, FR_FMA(ar, br, zr));
+    zi = FR_FMA(ai, br, FR_FMA(ar, bi, zi));
+}
+// forward butterfly: t = c * hi; (lo, hi) <- (lo + t, lo - t)
+FR_HD void fwd_bf(double& xr, double& xi, double& yr, double& yi, double cr, double ci) {
+    double tr, ti;
+    cmul(cr, ci, yr, yi, tr, ti);
+    yr = xr - tr;
+    yi = xi - ti;
+    xr = xr + tr;
+    xi = xi + ti;
+}
+// inverse butterfly: d = u - v; (u, v) <- (u + v, conj(c) * d)
+//   conj(c) d: re = fma(c.re, d.re, c.im d.im), im = fma(c.re, d.im, -(c.im d.re))
+FR_HD void inv_bf(double& ur, double& ui, double& vr, double& vi, double cr, double ci) {
+    const double dr = ur - vr, di = ui - vi;
+    ur = ur + vr;
+    ui = ui + vi;
+    const double pr = ci * di, pi = -(ci * dr);
+    vr = FR_FMA(cr, dr, pr);
+    vi = FR_FMA(cr, di, pi);
+}
+// psi^k (k in [0, 2N)) from the quadrant table qt[r] = psi^r, r < N/2:
+// psi^k = i^(k / (N/2)) psi^(k mod N/2); i * (a + bi) = -b + ai.
+FR_HD void psi_quadrant(double ar, double ai, uint32_t q, double& zr, double& zi) {
+    if (q & 1) {
+        const double t = ar;
+        ar = -ai;
+        ai = t;
+    }
+    if (q & 2) {
+        ar = -ar;
+        ai = -ai;
+    }
+    zr = ar;
+    zi = ai;
+}
+// f64 (an integer-valued approximation, |v| < 2^100) -> v mod 2^64, exact:
+// k = rint(v / 2^64); r = v - k 2^64 (exact, |r| <= 2^63); ri = rint(r);
+// ri = hi 2^32 + lo with hi = floor(ri / 2^32), lo in [0, 2^32).
+FR_HD uint64_t torus_of(double v) {
+#if defined(__HIPCC__)
+    const double k = __builtin_rint(v * 0x1p-64);
+    const double ri = __builtin_rint(FR_FMA(-k, 0x1p64, v));
+    const double hi = __builtin_floor(ri * 0x1p-32);
+#else
+    const double k = std::nearbyint(v * 0x1p-64);
+    const double ri = std::nearbyint(FR_FMA(-k, 0x1p64, v));
+    const double hi = std::floor(ri * 0x1p-32);
+#endif
+    const double lo = FR_FMA(-hi, 0x1p32, ri);
+    const double hu = hi < 0 ? hi + 0x1p32 : hi;
+    return ((uint64_t)(uint32_t)hu << 32) + (uint64_t)(uint32_t)lo;
+}
+// signed gadget digit of a torus value: base 2^B, one level (B = pbs_base_log),
+// closest multiple of 2^(64-B) (round half up), digit in [-2^(B-1), 2^(B-1))
+template <int B>
+FR_HD int32_t pbs_digit(uint64_t a) {
+    const uint64_t c = ((a >> (64 - B)) + ((a >> (63 - B)) & 1)) & ((1ULL << B) - 1);
+    return c >= (1ULL << (B - 1)) ? (int32_t)c - (1 << B) : (int32_t)c;
+}
+
+// ---------------------------------------------------------------- host side
+// psi^x (x mod 2N) = i^q (cos(pi r / N), sin(pi r / N)), x = q N/2 + r
+c64 psi_pow(int N, int64_t x);
+
+struct Tables {
+    int N = 0, M = 0, LOG = 0;
+    std::vector<c64> tw;      // [M]: tw[(1 << s) + b] = psi^(E(s,b)/2); tw[0] unused
+    std::vector<c64> qt;      // [N/2]: psi^r
+    std::vector<uint16_t> leaf;  // [M]: L(j) = E(LOG, j) mod 2N
+    explicit Tables(int N);
+    void forward(c64* z) const;   // natural order -> slot order (M points)
+    void inverse(c64* z) const;   // slot order -> natural order, times M
+};
+
+// Fourier bootstrapping key: every GGSW polynomial of the torus BSK
+// ([w][r][c][coef] u64) folded, transformed and scaled by 1/M, as
+// [w][r][c][slot] complex.
+void bsk_to_fourier(const Tables& T, const std::vector<uint64_t>& bsk, size_t polys, std::vector<c64>& out);
+
+}  // namespace fft
+}  // namespace fr

@@ -1,0 +1,408 @@
+// Blind rotation on the 2^64 torus with an f64 negacyclic FFT (FR_RING_FFT),
+// gfx950.  The ring, the transform and every floating-point operation are
+// specified in fft.h; oracle/tfhe_oracle.c restates the same sequence.
+// (File named fft_br.hip so its object does not collide with fft.cpp.)
+//
+//   k_blind_rotate_fft<N,E>: modulus switch, test-polynomial accumulator (u64),
+//     the unrolled blind rotation (k = 1: one step per pair of LWE
+//     coefficients, three GGSWs, see device.hip), multi-value w-step and
+//     sample extract -- outputs are already torus LWEs, no ring conversion.
+//
+// Geometry: one workgroup per bootstrap, 2 * M/E lanes (M = N/2 complex
+// points per polynomial, E per lane, whole waves per polynomial).  The
+// log2 M transform stages run as register phases of log2 E stages joined by
+// LDS exchanges of 16-B complex values (conflict-free maps of geo.h with
+// 8-lane b128 groups).  Per step a lane: gadget digits of its 2E accumulator
+// coefficients (local, exact), forward FFT, MAC with the three Fourier GGSWs
+// (coalesced [w][r][c][m][lane] layout) and their slot-wise monomial factors
+// psi^(e L) - 1 (quadrant table in LDS), inverse FFT, exact f64 -> torus
+// conversion and u64 accumulate.
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+
+#include "device.h"
+#include "fft.h"
+#include "geo.h"
+
+namespace fr {
+
+#define FFT_CHECK(x)                                                                         \
+    do {                                                                                     \
+        hipError_t _e = (x);                                                                 \
+        if (_e != hipSuccess)                                                                \
+            throw Error(FR_ERR_HIP, std::string("HIP error: ") + hipGetErrorString(_e) +     \
+                                        " at " __FILE__ ":" + std::to_string(__LINE__));     \
+    } while (0)
+
+template <int M, int E>
+using FGeo = NttGeo<M, E, 3>;
+
+__device__ __forceinline__ void cfwd(double2& x, double2& y, double2 c) { fft::fwd_bf(x.x, x.y, y.x, y.y, c.x, c.y); }
+__device__ __forceinline__ void cinv(double2& u, double2& v, double2 c) { fft::inv_bf(u.x, u.y, v.x, v.y, c.x, c.y); }
+
+template <int M, int E, int p>
+__device__ __forceinline__ void ffwd_phase(double2 (&x)[E], const double2* tw, int tl) {
+    using G = FGeo<M, E>;
+    const int b = G::template base<p>(tl);
+#pragma unroll
+    for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+        const double2* zs = tw + (b >> (G::LOG - s));
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            cfwd(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))]);
+        }
+    }
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, int tl) {
+    using G = FGeo<M, E>;
+    const int b = G::template base<p>(tl);
+#pragma unroll
+    for (int s = G::s_end(p) - 1; s >= G::s_begin(p); --s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+        const double2* zs = tw + (b >> (G::LOG - s));
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            cinv(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))]);
+        }
+    }
+}
+
+// exchange between phase layouts stays inside each wave (see device.hip)
+template <int M, int E, int PF, int PT>
+constexpr bool fwave_local() {
+    using G = FGeo<M, E>;
+    for (int b = 6; (1 << b) < G::T; ++b) {
+        const int f = b < G::lo(PF) ? b : b + G::e, t = b < G::lo(PT) ? b : b + G::e;
+        if (f != t) return false;
+    }
+    return true;
+}
+__device__ __forceinline__ void fwave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+template <int M, int E, int PF, int PT, bool PRE>
+__device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
+    using G = FGeo<M, E>;
+    constexpr int X = PF < PT ? PF : PT;
+    double2* rf = row + G::template at<X>(G::template base<PF>(tl));
+    double2* rt = row + G::template at<X>(G::template base<PT>(tl));
+    if constexpr (PRE) __syncthreads();
+#pragma unroll
+    for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+    if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
+    else __syncthreads();
+#pragma unroll
+    for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
+}
+// barrier plan as in device.hip: only the first exchange of a transform and
+// exchanges writing a non-wave-top layout wait before writing
+template <int M, int E, int p>
+constexpr bool ffwd_pre() {
+    return p == 0 || !FGeo<M, E>::wave_top(p);
+}
+template <int M, int E, int p>
+constexpr bool finv_pre() {
+    return p == FGeo<M, E>::NPH - 1 || !FGeo<M, E>::wave_top(p);
+}
+template <int M, int E, int X = 0>
+constexpr bool fexchanges_conflict_free() {
+    using G = FGeo<M, E>;
+    if constexpr (X + 1 >= G::NPH) return true;
+    else return G::template banks_distinct<X>(X) && G::template banks_distinct<X>(X + 1) &&
+                fexchanges_conflict_free<M, E, X + 1>();
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
+    ffwd_phase<M, E, p>(x, tw, tl);
+    if constexpr (p + 1 < FGeo<M, E>::NPH) {
+        fexchange<M, E, p, p + 1, ffwd_pre<M, E, p>()>(x, row, tl);
+        fforward_from<M, E, p + 1>(x, row, tw, tl);
+    }
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
+    finv_phase<M, E, p>(x, tw, tl);
+    if constexpr (p > 0) {
+        fexchange<M, E, p, p - 1, finv_pre<M, E, p>()>(x, row, tl);
+        finverse_from<M, E, p - 1>(x, row, tw, tl);
+    }
+}
+
+template <int N, int E>
+constexpr int fbr_threads() {
+    return 2 * (N / 2 / E);
+}
+template <int N, int E>
+constexpr size_t fbr_smem_bytes() {
+    return 16 * (2 * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (size_t)N / 2) + 16 * MAX_OUT + 2 * 1026 +
+           4 * 17 * MAX_OUT;
+}
+// 2 workgroups (each <= 80 KB of LDS) per CU: E = 4 -> 16 waves, 128 VGPRs
+template <int E>
+constexpr int fbr_min_waves() {
+    return E == 4 ? 4 : 2;
+}
+
+// value of the test polynomial at position t < N: the LUT polynomial (box N/16,
+// recentred by half a box, -f(0) in the last half box) or (Delta/2) * sum X^j
+template <int N>
+__device__ __forceinline__ uint64_t test_poly(int t, bool direct, const uint8_t* lut0) {
+    constexpr int box = N / 16, half = box / 2;
+    if (!direct) return 1ULL << (DELTA_LOG - 1);
+    const int mm = (t + half) / box;
+    return mm < 16 ? (uint64_t)lut0[mm] << DELTA_LOG : (uint64_t)0 - ((uint64_t)lut0[0] << DELTA_LOG);
+}
+// sum_t d_t (X^pos_t A)[j] mod 2^64 (multi-value w-step, terms as device.hip)
+template <int N>
+__device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t* terms, int nt, int j) {
+    uint64_t acc = 0;
+    for (int t = 0; t < nt; ++t) {
+        const uint32_t tm = terms[t];
+        int src = j - (int)(tm & 0xFFFF);
+        int64_t d = (int64_t)(tm >> 16) - 128;
+        if (src < 0) {
+            src += N;
+            d = -d;
+        }
+        acc += (uint64_t)d * row[src];
+    }
+    return acc;
+}
+
+template <int N, int E>
+__global__ void __launch_bounds__((fbr_threads<N, E>()), fbr_min_waves<E>())
+k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
+                   const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ qt_g,
+                   const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena, int slot_stride) {
+    constexpr int M = N / 2;
+    using G = FGeo<M, E>;
+    static_assert(fexchanges_conflict_free<M, E>(), "LDS maps must make every exchange conflict-free");
+    constexpr int T = M / E, NT = 2 * T, LAST = G::NPH - 1, XL = G::XL;
+    constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
+    extern __shared__ __attribute__((aligned(16))) double2 fsm[];
+    double2* xbuf = fsm;                  // 2 rows of NP complex: row P at P * NP
+    double2* tw = xbuf + 2 * G::NP;       // M forward twiddles
+    double2* qt = tw + M;                 // N/2: psi^r
+    uint8_t* lut = (uint8_t*)(qt + N / 2);             // 16 * n_out
+    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
+    uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
+    int* wcnt = (int*)(wterms + 16 * MAX_OUT);
+
+    const int tid = threadIdx.x;
+    const int P = __builtin_amdgcn_readfirstlane(tid / T), tl = tid % T;  // wave-uniform polynomial
+    const int g = blockIdx.x;
+    const uint64_t* in = ks + (size_t)g * ks_stride;
+    const int n_out = gates[g].n_out;
+    const int kind = gates[g].direct;
+    for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
+    for (int i = tid; i < N / 2; i += NT) qt[i] = qt_g[i];
+    for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
+    for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
+    if (tid == 0) abar[n] = 0;  // pad an odd n
+    const uint32_t bbar = mod_switch(in[n], LOG2N2);
+    uint32_t Ls[E];  // leaf exponents of this lane's slots
+#pragma unroll
+    for (int m = 0; m < E; ++m) Ls[m] = leaf_g[G::template idx<LAST>(tl, m)];
+    __syncthreads();
+
+    // accumulator (u64 torus), natural order: lane holds coefficients j and j + M
+    // for j = idx<0>(tl, m); mask polynomial 0, body X^-bbar * V
+    uint64_t alo[E], ahi[E];
+    {
+        const bool direct = kind == JOB_DIRECT;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            uint64_t v[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int s = (j + h * M + (int)bbar) & (2 * N - 1);
+                const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut);
+                v[h] = s < N ? tv : (uint64_t)0 - tv;
+            }
+            alo[m] = P == 1 ? v[0] : 0;
+            ahi[m] = P == 1 ? v[1] : 0;
+        }
+    }
+
+    double2* row = xbuf + P * G::NP;
+    const double2* orow = xbuf + (1 - P) * G::NP;
+    const int bl = G::template base<LAST>(tl);
+    double2* row_bl = row + G::template at<XL>(bl);
+    const double2* orow_bl = orow + G::template at<XL>(bl);
+    constexpr size_t GG = 4 * (size_t)M;  // complex values per Fourier GGSW: [r][c][m][lane]
+    const double2* bsk_l = bsk + (size_t)P * M + tl;
+    const int steps = (n + 1) / 2;
+    for (int t = 0; t < steps; ++t) {
+        const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
+        if ((ai | aj) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
+        // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
+        double2 x[E];
+#pragma unroll
+        for (int m = 0; m < E; ++m)
+            x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
+        // 2. forward FFT
+        fforward_from<M, E, 0>(x, row, tw, tl);
+        // 3. MAC with the three GGSWs of the pair and their monomial factors
+#pragma unroll
+        for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
+        __syncthreads();
+        const uint32_t e[3] = {(uint32_t)__builtin_amdgcn_readfirstlane((ai + aj) & (2 * N - 1)),
+                               (uint32_t)__builtin_amdgcn_readfirstlane(ai), (uint32_t)__builtin_amdgcn_readfirstlane(aj)};
+        const double2* bw = bsk_l + (size_t)(3 * t) * GG;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const double2 oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
+            const double2 d0 = P == 0 ? x[m] : oth, d1 = P == 0 ? oth : x[m];
+            double zr = 0, zi = 0;
+#pragma unroll
+            for (int gg = 0; gg < 3; ++gg) {
+                const double2 B0 = bw[(size_t)gg * GG + (size_t)m * T];
+                const double2 B1 = bw[(size_t)gg * GG + 2 * (size_t)M + (size_t)m * T];
+                double yr, yi;
+                fft::cmul(d0.x, d0.y, B0.x, B0.y, yr, yi);
+                fft::cmac(d1.x, d1.y, B1.x, B1.y, yr, yi);
+                const uint32_t k = __umul24(e[gg], Ls[m]) & (2 * N - 1);
+                const double2 q = qt[k & (N / 2 - 1)];
+                double cr, ci;
+                fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), cr, ci);
+                cr = cr - 1.0;
+                if (gg == 0) fft::cmul(yr, yi, cr, ci, zr, zi);
+                else fft::cmac(yr, yi, cr, ci, zr, zi);
+            }
+            x[m] = make_double2(zr, zi);
+        }
+        // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
+        finverse_from<M, E, LAST>(x, row, tw, tl);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            alo[m] += fft::torus_of(x[m].x);
+            ahi[m] += fft::torus_of(x[m].y);
+        }
+    }
+
+    // publish the accumulator as u64 [P][N] over the exchange rows
+    __syncthreads();
+    uint64_t* accs = (uint64_t*)xbuf;
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        const int j = G::template idx<0>(tl, m);
+        accs[P * N + j] = alo[m];
+        accs[P * N + j + M] = ahi[m];
+    }
+    __syncthreads();
+    constexpr int K = 1, big = K * N;
+    if (kind != JOB_MULTI) {
+        uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
+        const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
+        for (int c = tid; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint64_t v = accs[pp * N + j];
+            out[c] = (t != 0 ? (uint64_t)0 - v : v) + (c == big ? post : 0);
+        }
+        return;
+    }
+    if (tid < n_out) {
+        // multi-value terms (device.hip lut_terms)
+        constexpr int box = N / 16, half = box / 2;
+        const uint8_t* lf = lut + 16 * tid;
+        uint32_t* terms = wterms + 16 * tid;
+        int nt = 0;
+        for (int tt = 1; tt <= 16; ++tt) {
+            const int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+            if (d != 0) terms[nt++] = (uint32_t)(tt < 16 ? tt * box - half : N - half) | ((uint32_t)(d + 128) << 16);
+        }
+        wcnt[tid] = nt;
+    }
+    __syncthreads();
+    for (int f = 0; f < n_out; ++f) {
+        const uint32_t* tf = wterms + 16 * f;
+        const int nt = wcnt[f];
+        uint64_t* out = arena + (size_t)gates[g].out_slot[f] * slot_stride;
+        for (int c = tid; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint64_t v = w_step64<N>(accs + pp * N, tf, nt, j);
+            out[c] = t != 0 ? (uint64_t)0 - v : v;
+        }
+    }
+}
+
+// ================================================================== host side
+static bool fft_supported(int N, int E) { return N == 2048 && (E == 4 || E == 8); }
+
+template <int N, int E>
+static void fft_attr() {
+    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)fbr_smem_bytes<N, E>()));
+}
+
+void Device::init_fft() {
+    if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
+    if (p_.k != 1 || !fft_supported(p_.N, fft_e_)) throw Error(FR_ERR_INVALID, "device: FFT ring needs k = 1, N = 2048, E in {4, 8}");
+    fft_attr<2048, 4>();
+    fft_attr<2048, 8>();
+    fft::Tables T(p_.N);
+    FFT_CHECK(hipMalloc(&d_ftw_, 16 * (size_t)T.M));
+    FFT_CHECK(hipMalloc(&d_fqt_, 16 * (size_t)(p_.N / 2)));
+    FFT_CHECK(hipMalloc(&d_fleaf_, 2 * (size_t)T.M));
+    FFT_CHECK(hipMemcpy(d_ftw_, T.tw.data(), 16 * (size_t)T.M, hipMemcpyHostToDevice));
+    FFT_CHECK(hipMemcpy(d_fqt_, T.qt.data(), 16 * (size_t)(p_.N / 2), hipMemcpyHostToDevice));
+    FFT_CHECK(hipMemcpy(d_fleaf_, T.leaf.data(), 2 * (size_t)T.M, hipMemcpyHostToDevice));
+}
+
+void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
+    const int N = p_.N, M = N / 2, kp1 = p_.k + 1, E = fft_e_, T = M / E;
+    const size_t polys = p_.bsk_ggsw() * (size_t)kp1 * kp1;
+    fft::Tables tabs(N);
+    std::vector<fft::c64> four;
+    fft::bsk_to_fourier(tabs, bsk, polys, four);
+    // slot order -> per-lane order [poly][m][lane]: lane tl's element m is slot idx<LAST>(tl, m)
+    int e = 0;
+    while ((1 << e) < E) ++e;
+    const int L = geo_lo(tabs.LOG, e, (tabs.LOG + e - 1) / e - 1);
+    std::vector<fft::c64> lanes(four.size());
+    for (size_t pq = 0; pq < polys; ++pq)
+        for (int tl = 0; tl < T; ++tl)
+            for (int m = 0; m < E; ++m) {
+                const int slot = (((tl >> L) << (L + e)) | (tl & ((1 << L) - 1))) + (m << L);
+                lanes[pq * M + (size_t)m * T + tl] = four[pq * M + slot];
+            }
+    (void)hipFree(d_fbsk_);
+    d_fbsk_ = nullptr;
+    FFT_CHECK(hipMalloc(&d_fbsk_, 16 * lanes.size()));
+    FFT_CHECK(hipMemcpy(d_fbsk_, lanes.data(), 16 * lanes.size(), hipMemcpyHostToDevice));
+}
+
+void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream) {
+    const hipStream_t s = (hipStream_t)stream;
+    auto go = [&](auto ec) {
+        constexpr int E = decltype(ec)::value;
+        k_blind_rotate_fft<2048, E><<<(unsigned)n, fbr_threads<2048, E>(), fbr_smem_bytes<2048, E>(), s>>>(
+            d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)d_fbsk_, (const double2*)d_ftw_,
+            (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
+    };
+    if (fft_e_ == 4) go(std::integral_constant<int, 4>{});
+    else go(std::integral_constant<int, 8>{});
+    FFT_CHECK(hipGetLastError());
+}
+
+void Device::free_fft() {
+    (void)hipFree(d_fbsk_);
+    (void)hipFree(d_ftw_);
+    (void)hipFree(d_fqt_);
+    (void)hipFree(d_fleaf_);
+    d_fbsk_ = nullptr;
+    d_ftw_ = d_fqt_ = nullptr;
+    d_fleaf_ = nullptr;
+}
+
+}  // namespace fr

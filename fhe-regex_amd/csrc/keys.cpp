@@ -245,7 +245,45 @@ static uint64_t ggsw_msg(const Params& p, const ClientKey& ck, size_t w) {
     return g == 0 ? (si & sj) : g == 1 ? (si & (1 - sj)) : ((1 - si) & sj);
 }
 
+// Torus BSK (FR_RING_FFT): row r of GGSW w is a GLWE encryption of zero on the
+// 2^64 torus (mask uniform u64, body = sum_j A_j S_j + e, e ~ sigma_glwe 2^64),
+// plus m_w * 2^(64 - B) (the one-level gadget, B = pbs_base_log) on coefficient
+// 0 of component r.  A_j S_j (binary S) is summed exactly as rotations of A.
+static void gen_bsk_torus(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk) {
+    const int k = p.k, N = p.N;
+    const size_t kp1 = (size_t)k + 1, nw = p.bsk_ggsw();
+    const uint64_t gadget = 1ULL << (64 - p.pbs_base_log);
+    bsk.assign(p.bsk_len(), 0);
+    parallel_for((int)nw, [&](int i) {
+        Rng rm(seed, STREAM_BSK_MASK), rn(seed, STREAM_BSK_NOISE);
+        const uint64_t msg = ggsw_msg(p, ck, (size_t)i);
+        for (size_t r = 0; r < kp1; ++r) {
+            uint64_t* row = bsk.data() + ((size_t)i * kp1 + r) * kp1 * N;
+            uint64_t* Bp = row + (size_t)k * N;
+            for (int j = 0; j < k; ++j) {
+                uint64_t* A = row + (size_t)j * N;
+                const uint64_t base = (((uint64_t)i * kp1 + r) * k + j) * N;
+                for (int t = 0; t < N; ++t) A[t] = rm.u64(base + t);
+                const uint64_t* S = ck.s_big.data() + (size_t)j * N;
+                for (int u = 0; u < N; ++u) {
+                    if (!S[u]) continue;
+                    // X^u A: coefficient t + u gets A[t] (t + u < N), -A[t] past the wrap
+                    for (int t = 0; t < N - u; ++t) Bp[t + u] += A[t];
+                    for (int t = N - u; t < N; ++t) Bp[t + u - N] -= A[t];
+                }
+            }
+            const uint64_t nb = ((uint64_t)i * kp1 + r) * N;
+            for (int t = 0; t < N; ++t) Bp[t] += (uint64_t)rn.gaussian(nb + t, p.glwe_sigma);
+            if (msg) row[r * N] += gadget;
+        }
+    });
+}
+
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk) {
+    if (p.ring == FR_RING_FFT) {
+        gen_bsk_torus(p, ck, seed, bsk);
+        return;
+    }
     const int k = p.k, N = p.N;
     const size_t kp1 = (size_t)k + 1, nw = p.bsk_ggsw();
     bsk.assign(p.bsk_len(), 0);

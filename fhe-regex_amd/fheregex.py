@@ -57,7 +57,7 @@ class NoDevice(FheRegexError):
 class Params(C.Structure):
     _fields_ = [("k", C.c_int32), ("N", C.c_int32), ("n", C.c_int32), ("ks_base_log", C.c_int32),
                 ("ks_level", C.c_int32), ("pbs_base_log", C.c_int32), ("pbs_level", C.c_int32),
-                ("_pad", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
+                ("ring", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
 
 
 class MatchStats(C.Structure):
@@ -170,13 +170,18 @@ def _p(a: np.ndarray):
     return a.ctypes.data_as(u64p)
 
 
-def default_params(k: Optional[int] = None, N: Optional[int] = None) -> Params:
+RING_RNS, RING_FFT = 0, 1  # fheregex.h FR_RING_*
+
+
+def default_params(k: Optional[int] = None, N: Optional[int] = None, ring: Optional[int] = None) -> Params:
     p = Params()
     _check(lib().fr_default_params(C.byref(p)))
     if k is not None:
         p.k = k
     if N is not None:
         p.N = N
+    if ring is not None:
+        p.ring = ring
     return p
 
 

@@ -57,6 +57,12 @@ enum {
     FR_ERR_NON_ASCII = -8,    /* encrypt_str on non-ASCII content (ciphertext.rs:33-35) */
 };
 
+/* Ring of the blind rotation.  FR_RING_FFT: GLWE/GGSW on the
+ * 2^64 torus with an f64 negacyclic FFT (tfhe-rs's own representation);
+ * FR_RING_RNS: Z_Q[X]/(X^N+1), Q = 998244353 * 1004535809, exact NTTs.  The
+ * server key (fr_export_server_key) is a torus BSK for FFT, mod Q for RNS. */
+enum { FR_RING_RNS = 0, FR_RING_FFT = 1 };
+
 typedef struct fr_ctx fr_ctx;
 typedef uint32_t fr_ct; /* ciphertext handle: a radix (4 blocks), boolean (block 0 + zeros) or trivial */
 
@@ -68,7 +74,7 @@ typedef struct {
     int32_t ks_level;     /* 5 */
     int32_t pbs_base_log; /* 23 */
     int32_t pbs_level;    /* 1 */
-    int32_t _pad;
+    int32_t ring;         /* blind-rotation ring: FR_RING_RNS (0) or FR_RING_FFT (1) */
     double lwe_sigma;
     double glwe_sigma;
 } fr_params;

@@ -23,7 +23,7 @@ RNS_PRIMES = (998244353, 1004535809)
 class Params(C.Structure):
     _fields_ = [("k", C.c_int32), ("N", C.c_int32), ("n", C.c_int32), ("ks_base_log", C.c_int32),
                 ("ks_level", C.c_int32), ("pbs_base_log", C.c_int32), ("pbs_level", C.c_int32),
-                ("_pad", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
+                ("ring", C.c_int32), ("lwe_sigma", C.c_double), ("glwe_sigma", C.c_double)]
 
 
 class Gate(C.Structure):
@@ -92,6 +92,11 @@ def lib():
         L.or_lut_terms.argtypes = [C.c_int, C.POINTER(C.c_uint8), C.POINTER(C.c_int32), C.POINTER(C.c_int32)]
         L.or_lincomb.argtypes = [C.c_int, C.POINTER(Gate), u64p, u64p]
         L.or_gates.argtypes = [C.c_void_p, u64p, C.POINTER(Gate), C.c_size_t, u64p, C.POINTER(C.c_int32), u64p]
+        L.or_fft_ring_mul.argtypes = [C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64), C.POINTER(C.c_int64)]
+        L.or_fft_tables.argtypes = [C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint16)]
+        L.or_bsk_fourier.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
+        L.or_torus_of.restype = C.c_uint64
+        L.or_torus_of.argtypes = [C.c_double]
         L.or_num_threads.restype = C.c_int
         L.or_set_threads.argtypes = [C.c_int]
         _lib = L
@@ -129,23 +134,28 @@ def parse_client_key(blob: bytes) -> dict:
                 num_blocks=num_blocks)
 
 
-def params_from_key(key: dict, k: int | None = None, N: int | None = None) -> Params:
+RING_RNS, RING_FFT = 0, 1  # fheregex.h FR_RING_*
+
+
+def params_from_key(key: dict, k: int | None = None, N: int | None = None, ring: int = RING_RNS) -> Params:
     """Reference params (k=1, N=2048) or the k=2, N=1024 reinterpretation of the
-    same 2048-bit flattened GLWE key."""
+    same 2048-bit flattened GLWE key; ring: RING_RNS (Z_Q, NTT)
+    or RING_FFT (2^64 torus, f64 FFT as tfhe-rs)."""
     k = int(key["k"]) if k is None else k
     N = int(key["N"]) if N is None else N
     assert k * N == len(key["s_big"])
     return Params(k, N, int(key["n"]), int(key["ks_base_log"]), int(key["ks_level"]),
-                  int(key["pbs_base_log"]), int(key["pbs_level"]), 0, float(key["lwe_sigma"]),
+                  int(key["pbs_base_log"]), int(key["pbs_level"]), ring, float(key["lwe_sigma"]),
                   float(key["glwe_sigma"]))
 
 
 class Oracle:
     """Keys + helpers around liboracle for a parameter set."""
 
-    def __init__(self, key: dict, seed: int, k: int | None = None, N: int | None = None, with_bsk=True):
+    def __init__(self, key: dict, seed: int, k: int | None = None, N: int | None = None, with_bsk=True,
+                 ring: int = RING_RNS):
         self.key = key
-        self.P = params_from_key(key, k, N)
+        self.P = params_from_key(key, k, N, ring)
         self.seed = seed
         self.big = self.P.k * self.P.N
         self.n = self.P.n
@@ -160,6 +170,14 @@ class Oracle:
             self.bsk = np.zeros(L.or_bsk_len(C.byref(self.P)), dtype=np.uint64)
             L.or_keygen_bsk(C.byref(self.P), ptr(self.s_big), ptr(self.s_small), seed, ptr(self.bsk))
             self._pk = L.or_bsk_prepare(C.byref(self.P), ptr(self.bsk))
+
+    def bsk_fourier(self) -> np.ndarray:
+        """Fourier-domain BSK (torus ring): [w][r][c][slot] complex128, scaled by 1/M."""
+        assert self.P.ring == RING_FFT and self._pk
+        M = self.P.N // 2
+        out = np.zeros(len(self.bsk) // self.P.N * M * 2, dtype=np.float64)
+        lib().or_bsk_fourier(self._pk, ptr(out, C.c_double))
+        return out.view(np.complex128)
 
     def __del__(self):
         if getattr(self, "_pk", None):

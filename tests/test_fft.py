@@ -1,0 +1,227 @@
+"""FR_RING_FFT: the blind rotation on the 2^64 torus with an f64 negacyclic FFT
+(tfhe-rs's own ring representation, reference Cargo.lock:602-615 / 110-114).
+
+CPU: the oracle's FFT product against exact schoolbook products, the torus
+server key identical between the product's keygen and the oracle's, the
+oracle's blind rotation decrypting to the LUT values.  GPU: the device
+blind rotation (direct, multi-value, sign) and gate programs bit-exact
+against the oracle's restatement of the same operation sequence, and whole
+matches decrypting to the reference result."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+import fheregex as F
+import oracle_ffi as of
+import regex_oracle as ro
+from conftest import GOLDEN
+
+SEED = 42
+
+
+@pytest.fixture(scope="module")
+def oracle_fft(fixture_key):
+    return of.Oracle(fixture_key, seed=SEED, ring=of.RING_FFT)
+
+
+def fft_mul(a, b):
+    N = len(a)
+    out = np.zeros(N, dtype=np.int64)
+    p = lambda x: x.ctypes.data_as(C.POINTER(C.c_int64))
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    b = np.ascontiguousarray(b, dtype=np.int64)
+    of.lib().or_fft_ring_mul(N, p(a), p(b), p(out))
+    return out
+
+
+def schoolbook(a, b):
+    N = len(a)
+    out = [0] * N
+    for i in range(N):
+        ai = int(a[i])
+        if ai == 0:
+            continue
+        for j in range(N):
+            d = i + j
+            if d < N:
+                out[d] += ai * int(b[j])
+            else:
+                out[d - N] -= ai * int(b[j])
+    return np.array([((x + (1 << 63)) % (1 << 64)) - (1 << 63) for x in out], dtype=np.int64)
+
+
+@pytest.mark.parametrize("N,abits,bbits", [(16, 20, 10), (256, 22, 12), (2048, 22, 8)])
+def test_fft_product_exact_for_small_operands(N, abits, bbits):
+    """|a| |b| N < 2^50: the f64 FFT product rounds to the exact integer product."""
+    rng = np.random.default_rng(N)
+    a = rng.integers(-(1 << abits), 1 << abits, N, dtype=np.int64)
+    b = rng.integers(-(1 << bbits), 1 << bbits, N, dtype=np.int64)
+    if N == 2048:  # keep the schoolbook check fast: sparse a
+        a[rng.random(N) < 0.9] = 0
+    assert (fft_mul(a, b) == schoolbook(a, b)).all()
+
+
+def test_fft_monomial_is_a_rotation():
+    N = 64
+    rng = np.random.default_rng(3)
+    a = rng.integers(-(1 << 20), 1 << 20, N, dtype=np.int64)
+    for e in (0, 1, 17, 63):
+        b = np.zeros(N, dtype=np.int64)
+        b[e] = 1
+        exp = np.concatenate([-a[N - e:], a[:N - e]]) if e else a
+        assert (fft_mul(a, b) == exp).all(), e
+
+
+def test_fft_error_on_torus_sized_products():
+    """Digit-sized (2^22) times torus-sized (2^63) operands: the FFT result
+    modulo 2^64 stays within 2^44 of the exact product (the noise budget the
+    bootstrap relies on; tfhe-rs's FFT has the same error class)."""
+    N = 2048
+    rng = np.random.default_rng(5)
+    a = rng.integers(-(1 << 22), 1 << 22, N, dtype=np.int64)
+    a[rng.random(N) < 0.97] = 0
+    b = rng.integers(-(1 << 62), 1 << 62, N, dtype=np.int64)
+    err = (fft_mul(a, b) - schoolbook(a, b)).astype(np.int64)  # wraps mod 2^64
+    assert np.abs(err).max() < (1 << 44), int(np.abs(err).max()).bit_length()
+
+
+def test_torus_of_exact():
+    L = of.lib()
+    for v, e in [(0.0, 0), (-1.0, (1 << 64) - 1), (2.0**63, 1 << 63), (-(2.0**63), 1 << 63), (2.0**64 + 2**20, 1 << 20),
+                 (3 * 2.0**70 + 5 * 2.0**30, (5 << 30) % (1 << 64)), (-(2.0**80) - 2.0**40, ((1 << 64) - (1 << 40)))]:
+        assert L.or_torus_of(v) == e, (v, e)
+
+
+def test_torus_server_key_matches_oracle(key_blob, oracle_fft):
+    ctx = F.Context(device=-1, params=F.default_params(ring=F.RING_FFT))
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    ksk, bsk = ctx.export_server_key()
+    assert (ksk == oracle_fft.ksk).all()
+    assert (bsk == oracle_fft.bsk).all()
+
+
+def test_torus_ggsw_rows_encrypt_gadget_times_key_bit(oracle_fft, fixture_key):
+    """Row r of GGSW w decrypts (component phase) to m_w * 2^41 on component r's
+    coefficient 0 plus small noise."""
+    O = oracle_fft
+    N = O.P.N
+    s = O.s_big.astype(np.int64)
+    ss = O.s_small
+    for w in (0, 1, 2, 99):
+        t, g = divmod(w, 3)
+        si, sj = int(ss[2 * t]), int(ss[2 * t + 1])
+        m = [si & sj, si & (1 - sj), (1 - si) & sj][g]
+        for r in range(2):
+            row = O.bsk[(w * 2 + r) * 2 * N:(w * 2 + r + 1) * 2 * N].reshape(2, N)
+            A, B = row[0].astype(np.uint64), row[1].astype(np.uint64)
+            # phase = B - A*S (negacyclic), mod 2^64, computed exactly with Python ints on a few coefficients
+            for c in (0, 1, N - 1):
+                acc = int(B[c])
+                for u in np.nonzero(s)[0]:
+                    src = c - u
+                    acc -= int(A[src]) if src >= 0 else -int(A[src + N])
+                acc %= 1 << 64
+                # gadget on component r: +2^41 on the body (r = 1) is +2^41 in the
+                # phase; on the mask (r = 0) it is -2^41 * S_c
+                expect = (m << 41) if (c == 0 and r == 1) else (-(m << 41) * int(s[c]) if r == 0 else 0)
+                err = (acc - expect) % (1 << 64)
+                err = err - (1 << 64) if err >= 1 << 63 else err
+                assert abs(err) < 1 << 20, (w, r, c)
+
+
+@pytest.mark.parametrize("msgs", [[9, 3, 15, 0], [1, 2, 7, 12]])
+def test_oracle_fft_blind_rotation_decrypts(oracle_fft, msgs):
+    O = oracle_fft
+    ks = O.keyswitch(O.encrypt_blocks(msgs, seed=sum(msgs)))
+    lut = [(7 * m + 3) % 16 for m in range(16)]
+    for i, m in enumerate(msgs):
+        assert int(O.decode16(O.blind_rotate(ks[i], lut))[0]) == lut[m]
+    luts = [lut, [m % 4 for m in range(16)], [int(m == msgs[0]) for m in range(16)]]
+    got = O.blind_rotate_multi(ks[0], luts)
+    assert [int(x) for x in O.decode16(got)] == [l[msgs[0]] for l in luts]
+
+
+# ------------------------------------------------------------------- GPU
+@pytest.fixture(scope="module")
+def fctx(key_blob):
+    ctx = F.Context(device=0, params=F.default_params(ring=F.RING_FFT))
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    return ctx
+
+
+@pytest.mark.gpu
+def test_fft_device_info(fctx):
+    assert "ring=fft" in fctx.info()
+
+
+@pytest.mark.gpu
+def test_fft_blind_rotate_bit_exact(fctx, oracle_fft):
+    O = oracle_fft
+    msgs = [5, 12, 0, 9]
+    ks = O.keyswitch(O.encrypt_blocks(msgs, seed=31))
+    luts = [[(3 * m + 1) % 16 for m in range(16)], [int(m >= 4) for m in range(16)], [m ^ 5 for m in range(16)],
+            [15 - m for m in range(16)]]
+    got = fctx.dev_blind_rotate(ks, luts)
+    for i in range(len(msgs)):
+        exp = O.blind_rotate(ks[i], luts[i])
+        assert (got[i] == exp).all(), (i, int(np.count_nonzero(got[i] != exp)))
+        assert O.decode16(got[i])[0] == luts[i][msgs[i]]
+
+
+@pytest.mark.gpu
+def test_fft_blind_rotate_random_masks_bit_exact(fctx, oracle_fft):
+    """Uniformly random keyswitched LWEs (every mask coefficient nonzero with
+    high probability, all 2N rotation amounts exercised)."""
+    O = oracle_fft
+    rng = np.random.default_rng(8)
+    ks = rng.integers(0, 2**64 - 1, (3, O.n + 1), dtype=np.uint64, endpoint=True)
+    ks[2, : O.n // 2] = 0  # half of the steps skipped
+    luts = [[m for m in range(16)]] * 3
+    got = fctx.dev_blind_rotate(ks, luts)
+    for i in range(3):
+        assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i
+
+
+@pytest.mark.gpu
+def test_fft_multi_value_and_sign_bit_exact(fctx, oracle_fft):
+    O = oracle_fft
+    ks = O.keyswitch(O.encrypt_blocks([6, 13], seed=55))
+    luts = [[int(v == 6) for v in range(16)], [int(v in (6, 13)) for v in range(16)], [int(v >= 9) for v in range(16)],
+            [int(v == 13) for v in range(16)], [int(v % 2 == 0) for v in range(16)]]
+    for i, m in enumerate([6, 13]):
+        got = fctx.dev_blind_rotate_multi(ks[i], luts)
+        exp = O.blind_rotate_multi(ks[i], luts)
+        assert (got == exp).all(), i
+        assert [int(O.decode16(o)[0]) for o in got] == [l[m] for l in luts]
+        sg = fctx.dev_blind_rotate_multi(ks[i], [luts[0]], direct=2)
+        assert (sg == O.blind_rotate_multi(ks[i], [luts[0]], direct=2)).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern,content", [("/abc/", "xyabcz"), ("/^abc$/", "abc"), ("/a[b-d]c/", "zzacczz"),
+                                             ("/abc/", "xyabz!"), ("/the/i", "In ThE end")])
+def test_fft_has_match_decrypts_to_reference(fctx, pattern, content):
+    hs = fctx.upload_radix(fctx.encrypt_str(content, seed=4))
+    out, st = fctx.has_match(hs, pattern)
+    exp = ro.has_match(content, pattern)
+    assert fctx.decrypt_radix(fctx.download_radix(out)) == exp.result
+    assert (st.ct_ops, st.cache_hits) == (exp.ct_ops, exp.cache_hits)
+
+
+@pytest.mark.gpu
+def test_fft_metric_config_256_chars(fctx):
+    rng = np.random.default_rng(0)
+    s = list("".join(chr(c) for c in rng.integers(0x20, 0x7F, 256)))
+    s[200:203] = "abc"
+    s = "".join(s)
+    hs = fctx.upload_radix(fctx.encrypt_str(s, seed=9))
+    out, st = fctx.has_match(hs, "/abc/")
+    assert fctx.decrypt_radix(fctx.download_radix(out)) == 1
+    s2 = s.replace("abc", "abd")
+    hs2 = fctx.upload_radix(fctx.encrypt_str(s2, seed=10))
+    out2, _ = fctx.has_match(hs2, "/abc/")
+    assert fctx.decrypt_radix(fctx.download_radix(out2)) == ro.has_match(s2, "/abc/").result
