@@ -105,10 +105,13 @@ class Device {
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
     // FR_RING_FFT: Fourier BSK [w][r][c][m][lane] (complex f64, scaled by 1/M), twiddles,
     // psi quadrant table, leaf exponents (fft.h)
-    int fft_e_ = 8;
-    double* d_fbsk_ = nullptr;
+    int fft_e_ = 8;          // complex points per lane for large launches
+    int fft_e_small_ = 4;    // ... for launches of at most fft_small_ bootstraps (latency)
+    size_t fft_small_ = 256;
+    double* d_fbsk_ = nullptr;  // layout for E = 8
+    double* d_fbsk4_ = nullptr;  // layout for E = 4
     double* d_ftw_ = nullptr;
-    double* d_fqt_ = nullptr;
+    double* d_fqt_ = nullptr;   // psi^k, k < 2N
     uint16_t* d_fleaf_ = nullptr;
     uint64_t* d_arena_ = nullptr;
     size_t arena_cap_ = 0;

@@ -139,15 +139,26 @@ template <int N, int E>
 constexpr int fbr_threads() {
     return 2 * (N / 2 / E);
 }
+// Two launch shapes:
+//  * latency (E = 4, launches of at most one bootstrap per CU): 8 waves per
+//    bootstrap, one workgroup per CU, 256 VGPRs; the step's 3 x 2 x E Fourier
+//    GGSW slots are loaded at the top of the step (they land during the digits
+//    and the forward FFT) and the full psi^k table (k < 2N) sits in LDS.
+//  * throughput (E = 8): 4 waves per bootstrap, two workgroups per CU (~68 KB
+//    of LDS each) hide each other's barrier and load latency; GGSW slots are
+//    loaded in the MAC; psi^k from the quadrant table (k < N/2) + quarter turns.
+template <int E>
+constexpr bool fbr_latency() {
+    return E == 4;
+}
 template <int N, int E>
 constexpr size_t fbr_smem_bytes() {
-    return 16 * (2 * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (size_t)N / 2) + 16 * MAX_OUT + 2 * 1026 +
-           4 * 17 * MAX_OUT;
+    return 16 * (2 * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (fbr_latency<E>() ? 2 * (size_t)N : (size_t)N / 2)) +
+           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT;
 }
-// 2 workgroups (each <= 80 KB of LDS) per CU: E = 4 -> 16 waves, 128 VGPRs
 template <int E>
 constexpr int fbr_min_waves() {
-    return E == 4 ? 4 : 2;
+    return fbr_latency<E>() ? 2 : 2;
 }
 
 // value of the test polynomial at position t < N: the LUT polynomial (box N/16,
@@ -179,7 +190,7 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
 template <int N, int E>
 __global__ void __launch_bounds__((fbr_threads<N, E>()), fbr_min_waves<E>())
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
-                   const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ qt_g,
+                   const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ psi_g,
                    const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena, int slot_stride) {
     constexpr int M = N / 2;
     using G = FGeo<M, E>;
@@ -189,8 +200,10 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
     double2* xbuf = fsm;                  // 2 rows of NP complex: row P at P * NP
     double2* tw = xbuf + 2 * G::NP;       // M forward twiddles
-    double2* qt = tw + M;                 // N/2: psi^r
-    uint8_t* lut = (uint8_t*)(qt + N / 2);             // 16 * n_out
+    constexpr bool LAT = fbr_latency<E>();
+    constexpr int NPSI = LAT ? 2 * N : N / 2;
+    double2* psi = tw + M;                // psi^k, k < NPSI
+    uint8_t* lut = (uint8_t*)(psi + NPSI);             // 16 * n_out
     uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
     uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
     int* wcnt = (int*)(wterms + 16 * MAX_OUT);
@@ -202,7 +215,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const int n_out = gates[g].n_out;
     const int kind = gates[g].direct;
     for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
-    for (int i = tid; i < N / 2; i += NT) qt[i] = qt_g[i];
+    for (int i = tid; i < NPSI; i += NT) psi[i] = psi_g[i];
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
@@ -238,11 +251,23 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     double2* row_bl = row + G::template at<XL>(bl);
     const double2* orow_bl = orow + G::template at<XL>(bl);
     constexpr size_t GG = 4 * (size_t)M;  // complex values per Fourier GGSW: [r][c][m][lane]
-    const double2* bsk_l = bsk + (size_t)P * M + tl;
     const int steps = (n + 1) / 2;
+    // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other row][m]
+    double2 gv[3][2][LAT ? E : 1];
     for (int t = 0; t < steps; ++t) {
+        if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
+        // (uniform base pointers in SGPRs + the lane offset: no per-load address VGPRs)
+        const double2* bw = bsk + (size_t)(3 * __builtin_amdgcn_readfirstlane(t)) * GG;
+        if constexpr (LAT) {  // lands during the digits and the forward FFT
+#pragma unroll
+            for (int gg = 0; gg < 3; ++gg)
+#pragma unroll
+                for (int m = 0; m < E; ++m) {
+                    gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
+                    gv[gg][1][m] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+                }
+        }
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
-        if ((ai | aj) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
         // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
         double2 x[E];
 #pragma unroll
@@ -254,30 +279,47 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
         __syncthreads();
-        const uint32_t e[3] = {(uint32_t)__builtin_amdgcn_readfirstlane((ai + aj) & (2 * N - 1)),
-                               (uint32_t)__builtin_amdgcn_readfirstlane(ai), (uint32_t)__builtin_amdgcn_readfirstlane(aj)};
-        const double2* bw = bsk_l + (size_t)(3 * t) * GG;
+        // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j
+        const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            const double2 oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
-            const double2 d0 = P == 0 ? x[m] : oth, d1 = P == 0 ? oth : x[m];
-            double zr = 0, zi = 0;
+            const double2 own = x[m], oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
+            double cr[3], ci[3];
+#pragma unroll
+            for (int h = 1; h < 3; ++h) {
+                const uint32_t k = __umul24(h == 1 ? ei : ej, Ls[m]) & (2 * N - 1);
+                if constexpr (LAT) {
+                    const double2 c = psi[k];
+                    cr[h] = c.x;
+                    ci[h] = c.y;
+                } else {
+                    const double2 q = psi[k & (N / 2 - 1)];
+                    fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), cr[h], ci[h]);
+                }
+            }
+            fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
+            double zr, zi;
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
-                const double2 B0 = bw[(size_t)gg * GG + (size_t)m * T];
-                const double2 B1 = bw[(size_t)gg * GG + 2 * (size_t)M + (size_t)m * T];
+                // y_g = D_P B_g[P][P] + D_(1-P) B_g[1-P][P]  (own row first)
+                double2 Bo, Bx;
+                if constexpr (LAT) {
+                    Bo = gv[gg][0][LAT ? m : 0];
+                    Bx = gv[gg][1][LAT ? m : 0];
+                } else {
+                    Bo = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
+                    Bx = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+                }
                 double yr, yi;
-                fft::cmul(d0.x, d0.y, B0.x, B0.y, yr, yi);
-                fft::cmac(d1.x, d1.y, B1.x, B1.y, yr, yi);
-                const uint32_t k = __umul24(e[gg], Ls[m]) & (2 * N - 1);
-                const double2 q = qt[k & (N / 2 - 1)];
-                double cr, ci;
-                fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), cr, ci);
-                cr = cr - 1.0;
-                if (gg == 0) fft::cmul(yr, yi, cr, ci, zr, zi);
-                else fft::cmac(yr, yi, cr, ci, zr, zi);
+                fft::cmul(own.x, own.y, Bo.x, Bo.y, yr, yi);
+                fft::cmac(oth.x, oth.y, Bx.x, Bx.y, yr, yi);
+                if (gg == 0) fft::cmul(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
+                else fft::cmac(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
             }
             x[m] = make_double2(zr, zi);
+            // throughput shape: keep each slot's six loads in its own iteration
+            // (hoisting all 6E of them costs 24E VGPRs; the other workgroup hides the wait)
+            if constexpr (!LAT) __builtin_amdgcn_sched_barrier(0);
         }
         // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
         finverse_from<M, E, LAST>(x, row, tw, tl);
@@ -347,39 +389,50 @@ static void fft_attr() {
 
 void Device::init_fft() {
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
-    if (p_.k != 1 || !fft_supported(p_.N, fft_e_)) throw Error(FR_ERR_INVALID, "device: FFT ring needs k = 1, N = 2048, E in {4, 8}");
+    if (const char* ev = std::getenv("FR_FFT_SMALL_LANE_ELEMS")) fft_e_small_ = std::atoi(ev);
+    if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
+    if (p_.k != 1 || !fft_supported(p_.N, fft_e_) || !fft_supported(p_.N, fft_e_small_))
+        throw Error(FR_ERR_INVALID, "device: FFT ring needs k = 1, N = 2048, E in {4, 8}");
     fft_attr<2048, 4>();
+    static_assert(fbr_smem_bytes<2048, 8>() <= 80 * 1024, "throughput shape: two workgroups per CU");
     fft_attr<2048, 8>();
     fft::Tables T(p_.N);
     FFT_CHECK(hipMalloc(&d_ftw_, 16 * (size_t)T.M));
-    FFT_CHECK(hipMalloc(&d_fqt_, 16 * (size_t)(p_.N / 2)));
+    std::vector<fft::c64> psi(2 * (size_t)p_.N);
+    for (int k = 0; k < 2 * p_.N; ++k) psi[k] = fft::psi_pow(p_.N, k);
+    FFT_CHECK(hipMalloc(&d_fqt_, 16 * psi.size()));
     FFT_CHECK(hipMalloc(&d_fleaf_, 2 * (size_t)T.M));
     FFT_CHECK(hipMemcpy(d_ftw_, T.tw.data(), 16 * (size_t)T.M, hipMemcpyHostToDevice));
-    FFT_CHECK(hipMemcpy(d_fqt_, T.qt.data(), 16 * (size_t)(p_.N / 2), hipMemcpyHostToDevice));
+    FFT_CHECK(hipMemcpy(d_fqt_, psi.data(), 16 * psi.size(), hipMemcpyHostToDevice));
     FFT_CHECK(hipMemcpy(d_fleaf_, T.leaf.data(), 2 * (size_t)T.M, hipMemcpyHostToDevice));
 }
 
 void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
-    const int N = p_.N, M = N / 2, kp1 = p_.k + 1, E = fft_e_, T = M / E;
+    const int N = p_.N, M = N / 2, kp1 = p_.k + 1;
     const size_t polys = p_.bsk_ggsw() * (size_t)kp1 * kp1;
     fft::Tables tabs(N);
     std::vector<fft::c64> four;
     fft::bsk_to_fourier(tabs, bsk, polys, four);
-    // slot order -> per-lane order [poly][m][lane]: lane tl's element m is slot idx<LAST>(tl, m)
-    int e = 0;
-    while ((1 << e) < E) ++e;
-    const int L = geo_lo(tabs.LOG, e, (tabs.LOG + e - 1) / e - 1);
+    // slot order -> per-lane order [poly][m][lane] (one copy per lane geometry E):
+    // lane tl's element m is slot idx<LAST>(tl, m), so each load of a wave is 1 KB contiguous
     std::vector<fft::c64> lanes(four.size());
-    for (size_t pq = 0; pq < polys; ++pq)
-        for (int tl = 0; tl < T; ++tl)
-            for (int m = 0; m < E; ++m) {
-                const int slot = (((tl >> L) << (L + e)) | (tl & ((1 << L) - 1))) + (m << L);
-                lanes[pq * M + (size_t)m * T + tl] = four[pq * M + slot];
-            }
-    (void)hipFree(d_fbsk_);
-    d_fbsk_ = nullptr;
-    FFT_CHECK(hipMalloc(&d_fbsk_, 16 * lanes.size()));
-    FFT_CHECK(hipMemcpy(d_fbsk_, lanes.data(), 16 * lanes.size(), hipMemcpyHostToDevice));
+    for (int E : {8, 4}) {
+        const int T = M / E;
+        int e = 0;
+        while ((1 << e) < E) ++e;
+        const int L = geo_lo(tabs.LOG, e, (tabs.LOG + e - 1) / e - 1);
+        for (size_t pq = 0; pq < polys; ++pq)
+            for (int tl = 0; tl < T; ++tl)
+                for (int m = 0; m < E; ++m) {
+                    const int slot = (((tl >> L) << (L + e)) | (tl & ((1 << L) - 1))) + (m << L);
+                    lanes[pq * M + (size_t)m * T + tl] = four[pq * M + slot];
+                }
+        double*& dst = E == 8 ? d_fbsk_ : d_fbsk4_;
+        (void)hipFree(dst);
+        dst = nullptr;
+        FFT_CHECK(hipMalloc(&dst, 16 * lanes.size()));
+        FFT_CHECK(hipMemcpy(dst, lanes.data(), 16 * lanes.size(), hipMemcpyHostToDevice));
+    }
 }
 
 void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream) {
@@ -387,20 +440,23 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
     auto go = [&](auto ec) {
         constexpr int E = decltype(ec)::value;
         k_blind_rotate_fft<2048, E><<<(unsigned)n, fbr_threads<2048, E>(), fbr_smem_bytes<2048, E>(), s>>>(
-            d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)d_fbsk_, (const double2*)d_ftw_,
+            d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_), (const double2*)d_ftw_,
             (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
     };
-    if (fft_e_ == 4) go(std::integral_constant<int, 4>{});
+    // small launches (at most one bootstrap per CU): more waves per bootstrap for latency
+    const int E = n <= fft_small_ ? fft_e_small_ : fft_e_;
+    if (E == 4) go(std::integral_constant<int, 4>{});
     else go(std::integral_constant<int, 8>{});
     FFT_CHECK(hipGetLastError());
 }
 
 void Device::free_fft() {
     (void)hipFree(d_fbsk_);
+    (void)hipFree(d_fbsk4_);
     (void)hipFree(d_ftw_);
     (void)hipFree(d_fqt_);
     (void)hipFree(d_fleaf_);
-    d_fbsk_ = nullptr;
+    d_fbsk_ = d_fbsk4_ = nullptr;
     d_ftw_ = d_fqt_ = nullptr;
     d_fleaf_ = nullptr;
 }
