@@ -40,14 +40,15 @@ def algorithmic_bytes_per_pbs(p) -> int:
     return p.n * (p.k + 1) ** 2 * p.pbs_level * p.N * 8
 
 
-def cpu_baseline(params_name: str, sample: int):
-    """Time the oracle (CPU restatement, test infrastructure) on this host."""
+def cpu_baseline(params_name: str, sample: int, ring: int):
+    """Time the oracle (CPU restatement, test infrastructure) on this host, on
+    the same ring as the GPU run."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_ffi as of
 
     key = of.load_fixture_key()
     k, N = (1, 2048) if params_name == "k1n2048" else (2, 1024)
-    O = of.Oracle(key, seed=SERVER_KEY_SEED, k=k, N=N)
+    O = of.Oracle(key, seed=SERVER_KEY_SEED, k=k, N=N, ring=ring)
     threads = of.lib().or_num_threads()
     blocks = O.encrypt_blocks([i % 4 for i in range(2 * sample)], seed=5)
     lut = [int(v == 1) for v in range(16)]
@@ -60,7 +61,8 @@ def cpu_baseline(params_name: str, sample: int):
         "unit": "gate-bootstraps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} eq-nibble gate bootstraps (lincomb+KS+BR+SE, {params_name}) on the fixture key, "
+        "sample": f"{sample} eq-nibble gate bootstraps (lincomb+KS+BR+SE, {params_name}, "
+                  f"{'f64 FFT' if ring == of.RING_FFT else 'RNS NTT'} ring) on the fixture key, "
                   f"{threads} OpenMP threads, {dt:.1f} s",
     }
 
@@ -82,6 +84,8 @@ def main():
     ap.add_argument("--chars", type=int, default=256, help="content chars (start offsets) per GPU")
     ap.add_argument("--pattern", default="/abc/")
     ap.add_argument("--params", default="k1n2048", choices=["k1n2048", "k2n1024"])
+    ap.add_argument("--ring", default="auto", choices=["auto", "fft", "rns"],
+                    help="blind-rotation ring: f64-FFT torus (default for k1n2048) or the RNS NTT ring")
     ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"],
                     help="regex evaluation: the reference's enumeration, state merging, or auto")
     ap.add_argument("--content", default="printable", choices=["printable", "config5"],
@@ -117,7 +121,7 @@ def main():
         torch.cuda.synchronize()
 
     k, N = (1, 2048) if args.params == "k1n2048" else (2, 1024)
-    params = F.default_params(k=k, N=N)
+    params = F.default_params(k=k, N=N, ring={"auto": None, "fft": F.RING_FFT, "rns": F.RING_RNS}[args.ring])
     with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
         blob = f.read()
     ctx = F.Context(device, params)
@@ -244,9 +248,12 @@ def main():
 
     bpp = algorithmic_bytes_per_pbs(params)
     achieved_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
-    traffic, _ = load_traffic(os.path.join(REPO, "profiles", "r01", "pmc_summary.json"))
-    cpu = cpu_baseline(args.params, args.cpu_sample) if args.cpu_sample > 0 and world == 1 else None
+    traffic, tinfo = load_traffic(os.path.join(REPO, "profiles", "r01", "pmc_summary.json"))
+    if tinfo is not None and tinfo.get("ring", "rns") != ("fft" if params.ring == F.RING_FFT else "rns"):
+        traffic = None  # the PMC summary was measured on the other ring
+    cpu = cpu_baseline(args.params, args.cpu_sample, params.ring) if args.cpu_sample > 0 and world == 1 else None
     ms_per_step = elapsed / args.steps * 1e3
+    ring_name = "fft" if params.ring == F.RING_FFT else "rns"
     line = {
         "metric": METRIC,
         "value": total_rot / elapsed,
@@ -261,7 +268,8 @@ def main():
         "dtype": "u64",
         "data": "synthetic: seeded printable ASCII, real encryptions under the reference fixture client key",
         "config": {"workload": f"{args.pattern} contains-match, {args.chars} chars per GPU (start-offset shards)",
-                   "content_chars": L, "params": args.params, "lowering": args.lowering, "engine": args.engine,
+                   "content_chars": L, "params": args.params, "ring": ring_name, "lowering": args.lowering,
+                   "engine": args.engine,
                    "content": args.content,
                    "parallelism": f"start-offset shards x{world}"},
         "match_ms": ms_per_step,
@@ -279,7 +287,7 @@ def main():
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
             "traffic": traffic,
-            "kernel": "k_blind_rotate",
+            "kernel": "k_blind_rotate_fft" if params.ring == F.RING_FFT else "k_blind_rotate",
             "bytes_per_pbs": bpp,
             "br_launches": br_launches,
             "br_avg_ms": br_ms / max(br_launches, 1),

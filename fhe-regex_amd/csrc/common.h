@@ -58,7 +58,7 @@ struct Params {
     int k = 1, N = 2048, n = 742;
     int ks_base_log = 3, ks_level = 5;
     int pbs_base_log = 23, pbs_level = 1;
-    int ring = FR_RING_RNS;  // blind-rotation ring (fheregex.h)
+    int ring = FR_RING_FFT;  // blind-rotation ring (fheregex.h); k > 1 needs FR_RING_RNS
     double lwe_sigma = 7.069849454709433e-06;
     double glwe_sigma = 2.9403601535432533e-16;
     int big() const { return k * N; }

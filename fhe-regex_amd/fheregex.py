@@ -182,6 +182,8 @@ def default_params(k: Optional[int] = None, N: Optional[int] = None, ring: Optio
         p.N = N
     if ring is not None:
         p.ring = ring
+    elif (p.k, p.N) != (1, 2048):
+        p.ring = RING_RNS  # the FFT ring is built for the reference's k = 1, N = 2048
     return p
 
 

@@ -137,12 +137,15 @@ def parse_client_key(blob: bytes) -> dict:
 RING_RNS, RING_FFT = 0, 1  # fheregex.h FR_RING_*
 
 
-def params_from_key(key: dict, k: int | None = None, N: int | None = None, ring: int = RING_RNS) -> Params:
+def params_from_key(key: dict, k: int | None = None, N: int | None = None, ring: int | None = None) -> Params:
     """Reference params (k=1, N=2048) or the k=2, N=1024 reinterpretation of the
-    same 2048-bit flattened GLWE key; ring: RING_RNS (Z_Q, NTT)
-    or RING_FFT (2^64 torus, f64 FFT as tfhe-rs)."""
+    same 2048-bit flattened GLWE key; ring: RING_FFT (2^64
+    torus, f64 FFT as tfhe-rs; the product's default at k=1, N=2048) or
+    RING_RNS (Z_Q, NTT; the only ring for k > 1)."""
     k = int(key["k"]) if k is None else k
     N = int(key["N"]) if N is None else N
+    if ring is None:
+        ring = RING_FFT if (k, N) == (1, 2048) else RING_RNS
     assert k * N == len(key["s_big"])
     return Params(k, N, int(key["n"]), int(key["ks_base_log"]), int(key["ks_level"]),
                   int(key["pbs_base_log"]), int(key["pbs_level"]), ring, float(key["lwe_sigma"]),
@@ -153,7 +156,7 @@ class Oracle:
     """Keys + helpers around liboracle for a parameter set."""
 
     def __init__(self, key: dict, seed: int, k: int | None = None, N: int | None = None, with_bsk=True,
-                 ring: int = RING_RNS):
+                 ring: int | None = None):
         self.key = key
         self.P = params_from_key(key, k, N, ring)
         self.seed = seed

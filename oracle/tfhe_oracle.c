@@ -691,7 +691,6 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
         uint32_t ai = mod_switch(ks_lwe[i], log2N2);
         uint32_t aj = i + 1 < n ? mod_switch(ks_lwe[i + 1], log2N2) : 0;
         if (ai == 0 && aj == 0) continue;
-        uint32_t e[3] = {(ai + aj) % (2 * (uint32_t)N), ai, aj};
         for (size_t c = 0; c < kp1; c++) {
             cplx* Dc = D + c * M;
             for (int t = 0; t < M; t++) {
@@ -702,20 +701,26 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
         }
         for (size_t c = 0; c < kp1; c++) {
             for (int t = 0; t < M; t++) {
+                /* slot factors: psi^(a_i L), psi^(a_j L) from the quadrant table, and
+                 * their product for a_i + a_j */
+                double cr[3], ci[3];
+                for (int h = 1; h < 3; h++) {
+                    uint32_t kk = (uint32_t)(((uint64_t)(h == 1 ? ai : aj) * F->leaf[t]) % (2 * (uint64_t)N));
+                    cplx qv = F->qt[kk % (uint32_t)(N / 2)];
+                    quarter_turns(qv.re, qv.im, kk / (uint32_t)(N / 2), &cr[h], &ci[h]);
+                }
+                c_mul(cr[1], ci[1], cr[2], ci[2], &cr[0], &ci[0]);
                 double zr = 0, zi = 0;
                 for (int g = 0; g < 3; g++) {
                     const cplx* G = K->bsk_f + ((size_t)(i / 2) * 3 + g) * kp1 * kp1 * M;
+                    /* y_g = sum_r D_r G_g[r][c], the r = c term first */
                     double yr, yi;
-                    c_mul(D[t].re, D[t].im, G[(0 * kp1 + c) * M + t].re, G[(0 * kp1 + c) * M + t].im, &yr, &yi);
-                    for (size_t r = 1; r < kp1; r++)
-                        c_mac(D[r * M + t].re, D[r * M + t].im, G[(r * kp1 + c) * M + t].re, G[(r * kp1 + c) * M + t].im, &yr, &yi);
-                    uint32_t kk = (uint32_t)(((uint64_t)e[g] * F->leaf[t]) % (2 * (uint64_t)N));
-                    cplx qv = F->qt[kk % (uint32_t)(N / 2)];
-                    double cr, ci;
-                    quarter_turns(qv.re, qv.im, kk / (uint32_t)(N / 2), &cr, &ci);
-                    cr = cr - 1.0;
-                    if (g == 0) c_mul(yr, yi, cr, ci, &zr, &zi);
-                    else c_mac(yr, yi, cr, ci, &zr, &zi);
+                    c_mul(D[c * M + t].re, D[c * M + t].im, G[(c * kp1 + c) * M + t].re, G[(c * kp1 + c) * M + t].im, &yr, &yi);
+                    for (size_t r = 0; r < kp1; r++)
+                        if (r != c)
+                            c_mac(D[r * M + t].re, D[r * M + t].im, G[(r * kp1 + c) * M + t].re, G[(r * kp1 + c) * M + t].im, &yr, &yi);
+                    if (g == 0) c_mul(yr, yi, cr[g] - 1.0, ci[g], &zr, &zi);
+                    else c_mac(yr, yi, cr[g] - 1.0, ci[g], &zr, &zi);
                 }
                 Z[t].re = zr; Z[t].im = zi;
             }

@@ -30,6 +30,13 @@ def fixture_key():
 
 @pytest.fixture(scope="session")
 def oracle_k1(fixture_key):
-    """Oracle keys (k=1, N=2048) for server-key seed 42."""
+    """Oracle keys (k=1, N=2048, default ring: the f64-FFT torus) for server-key seed 42."""
     import oracle_ffi
     return oracle_ffi.Oracle(fixture_key, seed=42)
+
+
+@pytest.fixture(scope="session")
+def oracle_rns(fixture_key):
+    """Oracle keys on the RNS ring (Z_Q, two-prime NTT), k=1, N=2048, seed 42."""
+    import oracle_ffi
+    return oracle_ffi.Oracle(fixture_key, seed=42, ring=oracle_ffi.RING_RNS)

@@ -22,12 +22,19 @@ def load(name):
         return json.load(f)
 
 
-@pytest.fixture(scope="module")
-def gctx(key_blob):
-    ctx = F.Context(device=0)
+@pytest.fixture(scope="module", params=[F.RING_FFT, F.RING_RNS], ids=["fft", "rns"])
+def gctx(request, key_blob):
+    """Every test below runs on both blind-rotation rings."""
+    ctx = F.Context(device=0, params=F.default_params(ring=request.param))
     ctx.load_client_key(key_blob)
     ctx.gen_server_key(SEED)
     return ctx
+
+
+@pytest.fixture(scope="module")
+def oracle_k1(gctx, fixture_key):
+    """Oracle keys on the context's ring (server-key seed 42)."""
+    return of.Oracle(fixture_key, seed=SEED, ring=gctx.params.ring)
 
 
 def test_device_info(gctx):
@@ -35,6 +42,8 @@ def test_device_info(gctx):
 
 
 def test_ring_mul_bit_exact(gctx):
+    if gctx.params.ring != F.RING_RNS:
+        pytest.skip("ring-product test hook: RNS ring (the FFT product is covered by tests/test_fft.py)")
     rng = np.random.default_rng(1)
     P = of.Q_RING
     a = rng.integers(0, P, (3, 2048), dtype=np.uint64)

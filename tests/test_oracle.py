@@ -127,9 +127,14 @@ def test_encrypt_decrypt_roundtrip(oracle_k1):
     assert oracle_k1.decrypt_radix(t) == 1 + 2 * 4 + 3 * 16
 
 
-def test_oracle_pbs_lut(oracle_k1):
+@pytest.fixture(params=["fft", "rns"])
+def oracle_ring(request, oracle_k1, oracle_rns):
+    return oracle_k1 if request.param == "fft" else oracle_rns
+
+
+def test_oracle_pbs_lut(oracle_ring):
     """KS -> BR -> SE on fresh and trivial inputs decrypts to the LUT value."""
-    O = oracle_k1
+    O = oracle_ring
     msgs = [0, 5, 15, 9]
     blocks = O.encrypt_blocks(msgs, seed=21)
     blocks[3] = O.trivial_blocks([9])[0]
@@ -142,9 +147,9 @@ def test_oracle_pbs_lut(oracle_k1):
     assert (out[3][:-1] == 0).all()
 
 
-def test_oracle_multi_value_bootstrap(oracle_k1):
+def test_oracle_multi_value_bootstrap(oracle_ring):
     """One rotation of (Delta/2)*u serves several LUTs (w_f factorization)."""
-    O = oracle_k1
+    O = oracle_ring
     ks = O.keyswitch(O.encrypt_blocks([7, 0], seed=41))
     luts = [[int(v == 7) for v in range(16)], [int(v in (5, 7)) for v in range(16)], [int(v >= 3) for v in range(16)],
             [int(v == 0) for v in range(16)]]
@@ -170,9 +175,9 @@ def test_oracle_multi_value_bootstrap(oracle_k1):
         assert prod == V
 
 
-def test_oracle_sign_gate_fanin16(oracle_k1):
+def test_oracle_sign_gate_fanin16(oracle_ring):
     """Sign gates: OR/AND of 16 booleans in one bootstrap (offset in Delta/2 units)."""
-    O = oracle_k1
+    O = oracle_ring
     bits = [0] * 16
     ct = O.encrypt_blocks(bits, seed=61)
     ct1 = ct.copy()

@@ -51,7 +51,8 @@ def main():
     s_big, s_small = key["s_big"], key["s_small"]
     with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
         blob = f.read()
-    ctx = F.Context(0)
+    ring = {"fft": F.RING_FFT, "rns": F.RING_RNS}.get(os.environ.get("FR_RING", ""))
+    ctx = F.Context(0, params=F.default_params(ring=ring))
     ctx.load_client_key(blob)
     ctx.gen_server_key(42)
     rng = np.random.default_rng(1)
@@ -86,6 +87,7 @@ def main():
             errs.append(signed(phase(o[0], s_big) - np.uint64(int(msgs[i] >= 8) * DELTA)))
         res["sign"] = stats(np.array(errs))
     res["threshold_log2"] = 58.0
+    res["ring"] = "fft" if ctx.params.ring == F.RING_FFT else "rns"
     print(json.dumps(res, indent=1))
     if out_path:
         with open(out_path, "w") as f:

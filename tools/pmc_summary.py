@@ -57,7 +57,8 @@ def main():
     sat = max(launches, key=lambda e: e["grid"]) if launches else None
     match = [e for e in launches if e is not sat]
     per_launch = sum(e["hbm_bytes"] * e["calls"] for e in match) / max(1, sum(e["calls"] for e in match))
-    res = {"hbm_bytes_per_launch": per_launch, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the /abc/ match, averaged per launch",
+    ring = "fft" if any("blind_rotate_fft" in e.get("kernel", "") for e in launches) else "rns"
+    res = {"hbm_bytes_per_launch": per_launch, "ring": ring, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the /abc/ match, averaged per launch",
            "launches": launches}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
