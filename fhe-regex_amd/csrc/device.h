@@ -105,9 +105,8 @@ class Device {
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
     // FR_RING_FFT: Fourier BSK [w][r][c][m][lane] (complex f64, scaled by 1/M), twiddles,
     // psi quadrant table, leaf exponents (fft.h)
-    int fft_e_ = 8;          // complex points per lane for large launches
-    int fft_e_small_ = 4;    // ... for launches of at most fft_small_ bootstraps (latency)
-    size_t fft_small_ = 256;
+    int fft_e_ = 4;           // complex points per lane in the throughput shape (4 or 8; 4 measured faster)
+    size_t fft_small_ = 256;  // launches of at most this many bootstraps use the latency shape
     double* d_fbsk_ = nullptr;  // layout for E = 8
     double* d_fbsk4_ = nullptr;  // layout for E = 4
     double* d_ftw_ = nullptr;

@@ -991,7 +991,7 @@ std::string Device::info() const {
     (void)hipGetDeviceProperties(&prop, dev_);
     std::ostringstream o;
     o << prop.name << " " << prop.gcnArchName << " CUs=" << prop.multiProcessorCount;
-    if (p_.ring == FR_RING_FFT) o << " ring=fft E=" << fft_e_ << "/" << fft_e_small_;
+    if (p_.ring == FR_RING_FFT) o << " ring=fft E=" << fft_e_ << " latency<=" << fft_small_;
     else o << " ring=rns E=" << e_;
     return o.str();
 }

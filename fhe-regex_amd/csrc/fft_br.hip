@@ -118,20 +118,26 @@ constexpr bool fexchanges_conflict_free() {
     else return G::template banks_distinct<X>(X) && G::template banks_distinct<X>(X + 1) &&
                 fexchanges_conflict_free<M, E, X + 1>();
 }
-template <int M, int E, int p>
+// NOPRE: the rows of the forward transform + MAC and of the inverse transform
+// are separate buffers (latency shape).  Then no write needs a barrier before
+// it: a transform's first cross-wave write follows the previous cross-wave
+// exchange's barrier, which every wave reaches only after its last read of the
+// other buffer; the inverse's first write (own slots) no longer meets the other
+// polynomial's MAC reads.
+template <int M, int E, int p, bool NOPRE>
 __device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
     ffwd_phase<M, E, p>(x, tw, tl);
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
-        fexchange<M, E, p, p + 1, ffwd_pre<M, E, p>()>(x, row, tl);
-        fforward_from<M, E, p + 1>(x, row, tw, tl);
+        fexchange<M, E, p, p + 1, !NOPRE && ffwd_pre<M, E, p>()>(x, row, tl);
+        fforward_from<M, E, p + 1, NOPRE>(x, row, tw, tl);
     }
 }
-template <int M, int E, int p>
+template <int M, int E, int p, bool NOPRE>
 __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
     finv_phase<M, E, p>(x, tw, tl);
     if constexpr (p > 0) {
-        fexchange<M, E, p, p - 1, finv_pre<M, E, p>()>(x, row, tl);
-        finverse_from<M, E, p - 1>(x, row, tw, tl);
+        fexchange<M, E, p, p - 1, !NOPRE && finv_pre<M, E, p>()>(x, row, tl);
+        finverse_from<M, E, p - 1, NOPRE>(x, row, tw, tl);
     }
 }
 
@@ -139,26 +145,34 @@ template <int N, int E>
 constexpr int fbr_threads() {
     return 2 * (N / 2 / E);
 }
-// Two launch shapes:
-//  * latency (E = 4, launches of at most one bootstrap per CU): 8 waves per
-//    bootstrap, one workgroup per CU, 256 VGPRs; the step's 3 x 2 x E Fourier
-//    GGSW slots are loaded at the top of the step (they land during the digits
-//    and the forward FFT) and the full psi^k table (k < 2N) sits in LDS.
-//  * throughput (E = 8): 4 waves per bootstrap, two workgroups per CU (~68 KB
-//    of LDS each) hide each other's barrier and load latency; GGSW slots are
-//    loaded in the MAC; psi^k from the quadrant table (k < N/2) + quarter turns.
-template <int E>
-constexpr bool fbr_latency() {
-    return E == 4;
-}
-template <int N, int E>
+// Launch shapes (Device::launch_br_fft picks one by batch size):
+//  * latency, LAT (E = 4; launches of at most one bootstrap per CU): 8 waves,
+//    one workgroup per CU, 256 VGPRs; the step's 3 x 2 x E Fourier GGSW slots
+//    are loaded at the top of the step (they land during the digits and the
+//    forward FFT); the half psi^k table (k < N; psi^(k+N) = -psi^k) and two sets of exchange rows
+//    (forward + MAC / inverse: 3 barriers per step instead of 5) in LDS.
+//  * throughput (E = 4: 8 waves, 128 VGPRs; E = 8: 4 waves): two workgroups per
+//    CU (<= 80 KB of LDS each) hide each other's barriers and loads; a slot's
+//    GGSW values are loaded one slot ahead in the MAC; psi^k from the quadrant
+//    table (k < N/2) + quarter turns.
+template <int N, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
-    return 16 * (2 * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (fbr_latency<E>() ? 2 * (size_t)N : (size_t)N / 2)) +
+    return 16 * ((LAT ? 4 : 2) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (LAT ? (size_t)N : (size_t)N / 2)) +
            16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT;
 }
-template <int E>
+template <int E, bool LAT>
 constexpr int fbr_min_waves() {
-    return fbr_latency<E>() ? 2 : 2;
+    return LAT ? 2 : (E == 4 ? 4 : 2);
+}
+// the six Fourier GGSW values of slot m for this lane: [g][own row, other row]
+template <int M, int T>
+__device__ __forceinline__ void load_slot(double2 (&B)[3][2], const double2* bw, int P, int m, int tl) {
+    constexpr size_t GG = 4 * (size_t)M;
+#pragma unroll
+    for (int gg = 0; gg < 3; ++gg) {
+        B[gg][0] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
+        B[gg][1] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+    }
 }
 
 // value of the test polynomial at position t < N: the LUT polynomial (box N/16,
@@ -187,8 +201,8 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
     return acc;
 }
 
-template <int N, int E>
-__global__ void __launch_bounds__((fbr_threads<N, E>()), fbr_min_waves<E>())
+template <int N, int E, bool LAT>
+__global__ void __launch_bounds__((fbr_threads<N, E>()), (fbr_min_waves<E, LAT>()))
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
                    const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ psi_g,
                    const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena, int slot_stride) {
@@ -199,9 +213,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
     double2* xbuf = fsm;                  // 2 rows of NP complex: row P at P * NP
-    double2* tw = xbuf + 2 * G::NP;       // M forward twiddles
-    constexpr bool LAT = fbr_latency<E>();
-    constexpr int NPSI = LAT ? 2 * N : N / 2;
+    double2* ibuf = LAT ? xbuf + 2 * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
+    double2* tw = xbuf + (LAT ? 4 : 2) * G::NP;     // M forward twiddles
+    constexpr int NPSI = LAT ? N : N / 2;
     double2* psi = tw + M;                // psi^k, k < NPSI
     uint8_t* lut = (uint8_t*)(psi + NPSI);             // 16 * n_out
     uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
@@ -246,6 +260,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     }
 
     double2* row = xbuf + P * G::NP;
+    double2* irow = ibuf + P * G::NP;
     const double2* orow = xbuf + (1 - P) * G::NP;
     const int bl = G::template base<LAST>(tl);
     double2* row_bl = row + G::template at<XL>(bl);
@@ -274,24 +289,37 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int m = 0; m < E; ++m)
             x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
         // 2. forward FFT
-        fforward_from<M, E, 0>(x, row, tw, tl);
+        fforward_from<M, E, 0, LAT>(x, row, tw, tl);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
+        // throughput shapes: slot m's GGSW values, loaded one slot ahead (E = 8) or
+        // at the top of the slot (E = 4, 128 VGPRs: the other workgroup hides the wait)
+        constexpr bool AHEAD = !LAT && E == 8;
+        double2 Bc[3][2];
+        if constexpr (AHEAD) load_slot<M, T>(Bc, bw, P, 0, tl);
         __syncthreads();
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j
         const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
+            double2 Bn[3][2];
+            if constexpr (AHEAD) {
+                if (m + 1 < E) load_slot<M, T>(Bn, bw, P, m + 1, tl);
+                __builtin_amdgcn_sched_barrier(0);
+            } else if constexpr (!LAT) {
+                load_slot<M, T>(Bc, bw, P, m, tl);
+            }
             const double2 own = x[m], oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
             double cr[3], ci[3];
 #pragma unroll
             for (int h = 1; h < 3; ++h) {
                 const uint32_t k = __umul24(h == 1 ? ei : ej, Ls[m]) & (2 * N - 1);
-                if constexpr (LAT) {
-                    const double2 c = psi[k];
-                    cr[h] = c.x;
-                    ci[h] = c.y;
+                if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
+                    const double2 c = psi[k & (N - 1)];
+                    const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
+                    cr[h] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
+                    ci[h] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
                 } else {
                     const double2 q = psi[k & (N / 2 - 1)];
                     fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), cr[h], ci[h]);
@@ -302,14 +330,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
                 // y_g = D_P B_g[P][P] + D_(1-P) B_g[1-P][P]  (own row first)
-                double2 Bo, Bx;
-                if constexpr (LAT) {
-                    Bo = gv[gg][0][LAT ? m : 0];
-                    Bx = gv[gg][1][LAT ? m : 0];
-                } else {
-                    Bo = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
-                    Bx = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
-                }
+                const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
+                const double2 Bx = LAT ? gv[gg][1][LAT ? m : 0] : Bc[gg][1];
                 double yr, yi;
                 fft::cmul(own.x, own.y, Bo.x, Bo.y, yr, yi);
                 fft::cmac(oth.x, oth.y, Bx.x, Bx.y, yr, yi);
@@ -317,12 +339,20 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 else fft::cmac(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
             }
             x[m] = make_double2(zr, zi);
-            // throughput shape: keep each slot's six loads in its own iteration
-            // (hoisting all 6E of them costs 24E VGPRs; the other workgroup hides the wait)
-            if constexpr (!LAT) __builtin_amdgcn_sched_barrier(0);
+            if constexpr (!LAT) {
+                // keep the loads one slot ahead / in their slot, not all 6E hoisted (24E VGPRs)
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            if constexpr (AHEAD) {
+#pragma unroll
+                for (int gg = 0; gg < 3; ++gg) {
+                    Bc[gg][0] = Bn[gg][0];
+                    Bc[gg][1] = Bn[gg][1];
+                }
+            }
         }
         // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
-        finverse_from<M, E, LAST>(x, row, tw, tl);
+        finverse_from<M, E, LAST, LAT>(x, irow, tw, tl);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             alo[m] += fft::torus_of(x[m].x);
@@ -381,21 +411,23 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 // ================================================================== host side
 static bool fft_supported(int N, int E) { return N == 2048 && (E == 4 || E == 8); }
 
-template <int N, int E>
+template <int N, int E, bool LAT>
 static void fft_attr() {
-    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, E>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)fbr_smem_bytes<N, E>()));
+    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, E, LAT>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)fbr_smem_bytes<N, E, LAT>()));
 }
 
 void Device::init_fft() {
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
-    if (const char* ev = std::getenv("FR_FFT_SMALL_LANE_ELEMS")) fft_e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
-    if (p_.k != 1 || !fft_supported(p_.N, fft_e_) || !fft_supported(p_.N, fft_e_small_))
+    if (p_.k != 1 || !fft_supported(p_.N, fft_e_))
         throw Error(FR_ERR_INVALID, "device: FFT ring needs k = 1, N = 2048, E in {4, 8}");
-    fft_attr<2048, 4>();
-    static_assert(fbr_smem_bytes<2048, 8>() <= 80 * 1024, "throughput shape: two workgroups per CU");
-    fft_attr<2048, 8>();
+    static_assert(fbr_smem_bytes<2048, 4, true>() <= 160 * 1024, "latency shape: LDS");
+    static_assert(fbr_smem_bytes<2048, 4, false>() <= 80 * 1024 && fbr_smem_bytes<2048, 8, false>() <= 80 * 1024,
+                  "throughput shapes: two workgroups per CU");
+    fft_attr<2048, 4, true>();
+    fft_attr<2048, 4, false>();
+    fft_attr<2048, 8, false>();
     fft::Tables T(p_.N);
     FFT_CHECK(hipMalloc(&d_ftw_, 16 * (size_t)T.M));
     std::vector<fft::c64> psi(2 * (size_t)p_.N);
@@ -437,16 +469,19 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
 
 void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
-    auto go = [&](auto ec) {
+    auto go = [&](auto ec, auto lat) {
         constexpr int E = decltype(ec)::value;
-        k_blind_rotate_fft<2048, E><<<(unsigned)n, fbr_threads<2048, E>(), fbr_smem_bytes<2048, E>(), s>>>(
+        constexpr bool LAT = decltype(lat)::value;
+        k_blind_rotate_fft<2048, E, LAT><<<(unsigned)n, fbr_threads<2048, E>(), fbr_smem_bytes<2048, E, LAT>(), s>>>(
             d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_), (const double2*)d_ftw_,
             (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
     };
-    // small launches (at most one bootstrap per CU): more waves per bootstrap for latency
-    const int E = n <= fft_small_ ? fft_e_small_ : fft_e_;
-    if (E == 4) go(std::integral_constant<int, 4>{});
-    else go(std::integral_constant<int, 8>{});
+    using I4 = std::integral_constant<int, 4>;
+    using I8 = std::integral_constant<int, 8>;
+    // small launches (at most one bootstrap per CU): the latency shape
+    if (n <= fft_small_) go(I4{}, std::true_type{});
+    else if (fft_e_ == 4) go(I4{}, std::false_type{});
+    else go(I8{}, std::false_type{});
     FFT_CHECK(hipGetLastError());
 }
 
