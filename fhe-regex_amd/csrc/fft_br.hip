@@ -38,6 +38,23 @@ namespace fr {
 template <int M, int E>
 using FGeo = NttGeo<M, E, 3>;
 
+// FR_BR_TIMING (debug builds only): wave 0 of workgroup 0 accumulates
+// s_memtime deltas of the step segments and prints them at the end.
+#ifdef FR_BR_TIMING
+#define FBR_STAMP(k)                                            \
+    do {                                                        \
+        __builtin_amdgcn_sched_barrier(0);                      \
+        const uint64_t now_ = __builtin_amdgcn_s_memtime();     \
+        tseg[k] += now_ - tlast;                                \
+        tlast = now_;                                           \
+        __builtin_amdgcn_sched_barrier(0);                      \
+    } while (0)
+#else
+#define FBR_STAMP(k) \
+    do {             \
+    } while (0)
+#endif
+
 __device__ __forceinline__ void cfwd(double2& x, double2& y, double2 c) { fft::fwd_bf(x.x, x.y, y.x, y.y, c.x, c.y); }
 __device__ __forceinline__ void cinv(double2& u, double2& v, double2 c) { fft::inv_bf(u.x, u.y, v.x, v.y, c.x, c.y); }
 
@@ -234,9 +251,12 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
     const uint32_t bbar = mod_switch(in[n], LOG2N2);
-    uint32_t Ls[E];  // leaf exponents of this lane's slots
+    // leaf exponents mod 1024 of this lane's slot bases (slots 4b): L(j) = 1 + 4 brv(j)
+    // (fft::Tables::leaf, checked against the table in tests/test_fft.py)
+    uint32_t Lb[E / 4];
 #pragma unroll
-    for (int m = 0; m < E; ++m) Ls[m] = leaf_g[G::template idx<LAST>(tl, m)];
+    for (int bb = 0; bb < E / 4; ++bb)
+        Lb[bb] = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 4 * bb)) >> (32 - G::LOG))) & 1023u;
     __syncthreads();
 
     // accumulator (u64 torus), natural order: lane holds coefficients j and j + M
@@ -269,8 +289,14 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const int steps = (n + 1) / 2;
     // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other row][m]
     double2 gv[3][2][LAT ? E : 1];
+#ifdef FR_BR_TIMING
+    uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
+    uint64_t tlast = __builtin_amdgcn_s_memtime();
+    const uint64_t tstart = tlast;
+#endif
     for (int t = 0; t < steps; ++t) {
         if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
+        FBR_STAMP(0);
         // (uniform base pointers in SGPRs + the lane offset: no per-load address VGPRs)
         const double2* bw = bsk + (size_t)(3 * __builtin_amdgcn_readfirstlane(t)) * GG;
         if constexpr (LAT) {  // lands during the digits and the forward FFT
@@ -278,8 +304,13 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             for (int gg = 0; gg < 3; ++gg)
 #pragma unroll
                 for (int m = 0; m < E; ++m) {
+#ifdef FR_FFT_NOBSK  // timing experiment only (wrong results): no GGSW traffic
+                    gv[gg][0][m] = make_double2(t + gg, m);
+                    gv[gg][1][m] = make_double2(m, t - gg);
+#else
                     gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
                     gv[gg][1][m] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+#endif
                 }
         }
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
@@ -288,8 +319,10 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
         for (int m = 0; m < E; ++m)
             x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
+        FBR_STAMP(1);
         // 2. forward FFT
         fforward_from<M, E, 0, LAT>(x, row, tw, tl);
+        FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
@@ -299,8 +332,33 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         double2 Bc[3][2];
         if constexpr (AHEAD) load_slot<M, T>(Bc, bw, P, 0, tl);
         __syncthreads();
-        // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j
+        // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
+        // Slot m of this lane has L = Lb + 1024 s_m: Lb = L mod 1024 is shared by the
+        // slots of equal m >> 2 (E/4 bases per lane) and s_m = brv2(m & 3) (fft.h: L(j) =
+        // 1 + 4 brv(j)).  psi^(1024 s e) = i^(s e) is an exact quarter turn (the table
+        // itself is quadrant-reduced), so one lookup per (e, base) serves every slot.
         const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
+        constexpr int NB = E / 4;
+        double bre[2][NB], bim[2][NB];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+#pragma unroll
+            for (int bb = 0; bb < NB; ++bb) {
+                const uint32_t k = __umul24(h == 0 ? ei : ej, Lb[bb]) & (2 * N - 1);
+                if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
+#ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
+                    const double2 c = make_double2((double)k, 0.5);
+#else
+                    const double2 c = psi[k & (N - 1)];
+#endif
+                    const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
+                    bre[h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
+                    bim[h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
+                } else {
+                    const double2 q = psi[k & (N / 2 - 1)];
+                    fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h][bb], bim[h][bb]);
+                }
+            }
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             double2 Bn[3][2];
@@ -311,20 +369,11 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 load_slot<M, T>(Bc, bw, P, m, tl);
             }
             const double2 own = x[m], oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
+            const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
             double cr[3], ci[3];
 #pragma unroll
-            for (int h = 1; h < 3; ++h) {
-                const uint32_t k = __umul24(h == 1 ? ei : ej, Ls[m]) & (2 * N - 1);
-                if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
-                    const double2 c = psi[k & (N - 1)];
-                    const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
-                    cr[h] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
-                    ci[h] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
-                } else {
-                    const double2 q = psi[k & (N / 2 - 1)];
-                    fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), cr[h], ci[h]);
-                }
-            }
+            for (int h = 1; h < 3; ++h)  // uniform quarter turn
+                fft::psi_quadrant(bre[h - 1][m >> 2], bim[h - 1][m >> 2], ((h == 1 ? ei : ej) * sm) & 3u, cr[h], ci[h]);
             fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
             double zr, zi;
 #pragma unroll
@@ -351,14 +400,24 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 }
             }
         }
+        FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
         finverse_from<M, E, LAST, LAT>(x, irow, tw, tl);
+        FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             alo[m] += fft::torus_of(x[m].x);
             ahi[m] += fft::torus_of(x[m].y);
         }
+        FBR_STAMP(5);
     }
+#ifdef FR_BR_TIMING
+    if (blockIdx.x == 0 && tid == 0)
+        printf("FBR_TIMING E=%d LAT=%d steps=%d total=%lu digits=%lu fwd=%lu mac=%lu inv=%lu acc=%lu top=%lu\n", E, (int)LAT,
+               steps, (unsigned long)(__builtin_amdgcn_s_memtime() - tstart), (unsigned long)tseg[1],
+               (unsigned long)tseg[2], (unsigned long)tseg[3], (unsigned long)tseg[4], (unsigned long)tseg[5],
+               (unsigned long)tseg[0]);
+#endif
 
     // publish the accumulator as u64 [P][N] over the exchange rows
     __syncthreads();
