@@ -85,29 +85,32 @@ FR_HD void psi_quadrant(double ar, double ai, uint32_t q, double& zr, double& zi
     zr = ar;
     zi = ai;
 }
-// f64 (an integer-valued approximation, |v| < 2^100) -> v mod 2^64, exact:
-// k = rint(v / 2^64); r = v - k 2^64 (exact, |r| <= 2^63); ri = rint(r);
-// ri = hi 2^32 + lo with hi = floor(ri / 2^32), lo in [0, 2^32).
+// f64 (an integer-valued approximation, |v| < 2^100) -> rint(v) mod 2^64 (round
+// half to even), exact: ri = rint(v); hi = floor(ri / 2^32); lo = ri - hi 2^32 in
+// [0, 2^32); hi mod 2^32 = hi - floor(hi / 2^32) 2^32.  Every step is exact, so
+// this equals any other exact evaluation of rint(v) mod 2^64 (oracle/tfhe_oracle.c
+// reduces by 2^64 first).
 FR_HD uint64_t torus_of(double v) {
 #if defined(__HIPCC__)
-    const double k = __builtin_rint(v * 0x1p-64);
-    const double ri = __builtin_rint(FR_FMA(-k, 0x1p64, v));
+    const double ri = __builtin_rint(v);
     const double hi = __builtin_floor(ri * 0x1p-32);
+    const double hm = FR_FMA(-__builtin_floor(hi * 0x1p-32), 0x1p32, hi);
 #else
-    const double k = std::nearbyint(v * 0x1p-64);
-    const double ri = std::nearbyint(FR_FMA(-k, 0x1p64, v));
+    const double ri = std::nearbyint(v);
     const double hi = std::floor(ri * 0x1p-32);
+    const double hm = FR_FMA(-std::floor(hi * 0x1p-32), 0x1p32, hi);
 #endif
     const double lo = FR_FMA(-hi, 0x1p32, ri);
-    const double hu = hi < 0 ? hi + 0x1p32 : hi;
-    return ((uint64_t)(uint32_t)hu << 32) + (uint64_t)(uint32_t)lo;
+    return ((uint64_t)(uint32_t)hm << 32) | (uint64_t)(uint32_t)lo;
 }
 // signed gadget digit of a torus value: base 2^B, one level (B = pbs_base_log),
 // closest multiple of 2^(64-B) (round half up), digit in [-2^(B-1), 2^(B-1))
 template <int B>
 FR_HD int32_t pbs_digit(uint64_t a) {
-    const uint64_t c = ((a >> (64 - B)) + ((a >> (63 - B)) & 1)) & ((1ULL << B) - 1);
-    return c >= (1ULL << (B - 1)) ? (int32_t)c - (1 << B) : (int32_t)c;
+    // (a >> (64-B)) + bit (63-B), mod 2^B, recentred: on the high word, add half a
+    // digit unit and keep the top B bits as a signed field
+    static_assert(B >= 1 && B <= 31, "one-level digit inside the high word");
+    return (int32_t)((uint32_t)(a >> 32) + (1u << (31 - B))) >> (32 - B);
 }
 
 // ---------------------------------------------------------------- host side

@@ -63,6 +63,28 @@ def test_fft_product_exact_for_small_operands(N, abits, bbits):
     assert (fft_mul(a, b) == schoolbook(a, b)).all()
 
 
+def test_fft_tables_closed_forms():
+    """The kernel computes leaf exponents in closed form, L(j) = 1 + 4 brv(j) (the
+    slot of X^e's factor psi^(e L)); the twiddles are psi^((M >> (s+1)) (4 brv_s(b) + 1))
+    from the quadrant table, psi^(k + 1024 q) = i^q psi^k exactly."""
+    N, M = 2048, 1024
+    tw = np.zeros(2 * M)
+    qt = np.zeros(N)
+    leaf = np.zeros(M, dtype=np.uint16)
+    of.lib().or_fft_tables(N, tw.ctypes.data_as(C.POINTER(C.c_double)), qt.ctypes.data_as(C.POINTER(C.c_double)),
+                           leaf.ctypes.data_as(C.POINTER(C.c_uint16)))
+    brv = lambda x, b: int(format(x, "0%db" % b)[::-1], 2) if b else 0
+    assert all(int(leaf[j]) == 1 + 4 * brv(j, 10) for j in range(M))
+    twc, qtc = tw.view(np.complex128), qt.view(np.complex128)
+    for s in range(10):
+        for b in range(1 << s):
+            q, r = divmod(((M >> (s + 1)) * (4 * brv(b, s) + 1)) % (2 * N), N // 2)
+            z = qtc[r]
+            for _ in range(q):
+                z = complex(-z.imag, z.real)
+            assert twc[(1 << s) + b] == z, (s, b)
+
+
 def test_fft_monomial_is_a_rotation():
     N = 64
     rng = np.random.default_rng(3)
