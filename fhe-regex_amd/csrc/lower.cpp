@@ -6,6 +6,8 @@
 #include <map>
 #include <tuple>
 #include <cstring>
+#include <iterator>
+#include <unordered_map>
 
 namespace fr {
 
@@ -45,11 +47,30 @@ struct Form {
 
 inline int cblock(int pos, int blk) { return -(1 + pos * 4 + blk); }
 
+struct KeyHash {  // FNV-1a over the words of a gate key
+    size_t operator()(const std::vector<int64_t>& k) const {
+        uint64_t h = 1469598103934665603ULL;
+        for (int64_t w : k) h = (h ^ (uint64_t)w) * 1099511628211ULL;
+        return (size_t)h;
+    }
+};
+struct SetKey {
+    int pos;
+    std::bitset<256> set;
+    bool operator==(const SetKey& o) const { return pos == o.pos && set == o.set; }
+};
+struct SetKeyHash {
+    size_t operator()(const SetKey& k) const { return std::hash<std::bitset<256>>()(k.set) * 1000003u + (size_t)k.pos; }
+};
+
 struct Lowerer {
     const ValueDag& dag;
     int mode;
     Program prog;
-    std::map<std::vector<int64_t>, int> gate_index;  // hash-consing of gates
+    std::unordered_map<std::vector<int64_t>, int, KeyHash> gate_index;  // hash-consing of gates
+    // expand_set results by (position, set): lowering a set creates its gates once
+    // (later calls only hit gate_index), so the memo returns identical forms
+    std::unordered_map<SetKey, Form, SetKeyHash> set_memo;
     std::vector<Form> memo;
     std::vector<char> done;
 
@@ -88,10 +109,15 @@ struct Lowerer {
     //  * rows x cols <= 16: two class LUTs + one PBS on (cols*row + col);
     //  * otherwise OR over row classes of AND{[hi in class], [lo in L_class]}.
     Form lower_set(int pos, const std::bitset<256>& S) {
-        std::vector<std::bitset<16>> rowset(16);
-        for (int h = 0; h < 16; ++h)
-            for (int l = 0; l < 16; ++l)
-                if (S[h * 16 + l]) rowset[h][l] = 1;
+        // row h = bits 16h..16h+15 of S, read a 64-bit word at a time
+        std::bitset<16> rowset[16];
+        {
+            const std::bitset<256> m64(~0ull);
+            for (int w = 0; w < 4; ++w) {
+                const unsigned long long word = ((S >> (64 * w)) & m64).to_ullong();
+                for (int q = 0; q < 4; ++q) rowset[4 * w + q] = std::bitset<16>((word >> (16 * q)) & 0xFFFFu);
+            }
+        }
         // row classes: distinct non-empty lo-sets (class 0 = empty)
         std::vector<std::bitset<16>> rc;
         int rowcls[16];
@@ -126,7 +152,7 @@ struct Lowerer {
         int colcls[16];
         for (int l = 0; l < 16; ++l) {
             std::bitset<16> sig;
-            for (int h = 0; h < 16; ++h) sig[h] = S[h * 16 + l];
+            for (int h = 0; h < 16; ++h) sig[h] = rowset[h][l];
             int c = -1;
             for (size_t i = 0; i < cc.size(); ++i)
                 if (cc[i] == sig) c = (int)i;
@@ -174,6 +200,14 @@ struct Lowerer {
     Form expand_set(const Form& f) {
         if (f.set.none()) return const_form(0);
         if (f.set.all()) return const_form(1);
+        const SetKey key{f.pos, f.set};
+        auto it = set_memo.find(key);
+        if (it != set_memo.end()) return it->second;
+        Form r = expand_set_uncached(f);
+        set_memo.emplace(key, r);
+        return r;
+    }
+    Form expand_set_uncached(const Form& f) {
         Form a = lower_set(f.pos, f.set);
         if (a.k == Form::AND || a.k == Form::LIT) return a;
         Form b = negate(lower_set(f.pos, ~f.set));
@@ -255,9 +289,11 @@ struct Lowerer {
         // constant folding (booleans)
         if (a.k == Form::CONST) return is_and ? (a.c ? b : const_form(0)) : (a.c ? const_form(1) : b);
         if (b.k == Form::CONST) return is_and ? (b.c ? a : const_form(0)) : (b.c ? const_form(1) : a);
-        std::vector<Lit> l = members(a, is_and), r = members(b, is_and);
-        l.insert(l.end(), r.begin(), r.end());
-        std::sort(l.begin(), l.end());
+        // member lists are sorted (forms keep their literals sorted): merge, O(|a|+|b|)
+        const std::vector<Lit> l0 = members(a, is_and), r = members(b, is_and);
+        std::vector<Lit> l;
+        l.reserve(l0.size() + r.size());
+        std::merge(l0.begin(), l0.end(), r.begin(), r.end(), std::back_inserter(l));
         l.erase(std::unique(l.begin(), l.end()), l.end());
         for (size_t i = 0; i + 1 < l.size(); ++i)
             if (l[i].gate == l[i + 1].gate) return const_form(is_and ? 0 : 1);  // x & !x, x | !x
@@ -307,8 +343,11 @@ struct Lowerer {
                 case VNode::LE: {
                     f.k = Form::SET;
                     f.pos = n.pos;
-                    for (int ch = 0; ch < 256; ++ch)
-                        f.set[ch] = n.op == VNode::EQ ? ch == n.c : n.op == VNode::GT ? ch > n.c : ch <= n.c;
+                    // {c}, {ch > c} or {ch <= c}, built word-wise
+                    const std::bitset<256> all = std::bitset<256>().set();
+                    if (n.op == VNode::EQ) f.set.reset().set(n.c);
+                    else if (n.op == VNode::GT) f.set = all << (n.c + 1);
+                    else f.set = all >> (255 - n.c);
                     break;
                 }
                 case VNode::AND: f = combine(true, memo[n.a], memo[n.b]); break;

@@ -16,7 +16,7 @@ static double ms() { return std::chrono::duration<double, std::milli>(std::chron
 int main(int argc, char** argv) {
     const std::string pat = argc > 1 ? argv[1] : "/abc/";
     const size_t L = argc > 2 ? (size_t)std::atoi(argv[2]) : 256;
-    const int iters = 50;
+    const int iters = argc > 3 ? std::atoi(argv[3]) : 50;
     double tr = 0, tl = 0;
     size_t gates = 0;
     for (int it = 0; it < iters; ++it) {
