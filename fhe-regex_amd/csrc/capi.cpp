@@ -74,6 +74,7 @@ struct fr_ctx {
     std::vector<uint32_t> free_handles;
     int lowering = FR_LOWER_THRESHOLD;
     int engine = FR_ENGINE_AUTO;
+    int grammar = FR_GRAMMAR_REFERENCE;
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
 
     Device& device() {
@@ -255,6 +256,7 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
                         fr_match_stats* st) {
     double t0 = now_ms();
     ValueDag dag;
+    GrammarScope grammar(ctx->grammar);
     Recorded rec = record_has_match_engine(dag, n, pattern ? pattern : "", lo, hi, ctx->engine);
     Program prog = lower(dag, rec.root, ctx->lowering);
     double t1 = now_ms();
@@ -391,6 +393,13 @@ int fr_set_engine(fr_ctx* ctx, int32_t engine) {
     FR_TRY({
         NEED(ctx && engine >= FR_ENGINE_AUTO && engine <= FR_ENGINE_MERGED);
         ctx->engine = engine;
+    })
+}
+
+int fr_set_grammar(fr_ctx* ctx, int32_t grammar) {
+    FR_TRY({
+        NEED(ctx && (grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT));
+        ctx->grammar = grammar;
     })
 }
 
@@ -794,9 +803,13 @@ int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n, const char* 
 }
 
 int fr_parse(const char* pattern, char* buf, size_t len) {
+    return fr_parse_ex(pattern, FR_GRAMMAR_REFERENCE, buf, len);
+}
+
+int fr_parse_ex(const char* pattern, int32_t grammar, char* buf, size_t len) {
     FR_TRY({
         NEED(pattern && buf && len);
-        std::string s = to_string(*parse(pattern));
+        std::string s = to_string(*parse(pattern, grammar));
         if (s.size() + 1 > len) throw Error(FR_ERR_INVALID, "buffer too small");
         std::memcpy(buf, s.c_str(), s.size() + 1);
     })
@@ -804,10 +817,17 @@ int fr_parse(const char* pattern, char* buf, size_t len) {
 
 int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
                       int32_t engine, fr_plain_result* out) {
+    return fr_plain_match_g(content, len, pattern, lo, hi, lowering, engine, FR_GRAMMAR_REFERENCE, out);
+}
+
+int fr_plain_match_g(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                     int32_t engine, int32_t grammar, fr_plain_result* out) {
     FR_TRY({
         NEED((content || !len) && pattern && out && lo <= hi);
         NEED(engine >= FR_ENGINE_AUTO && engine <= FR_ENGINE_MERGED);
+        NEED(grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT);
         ValueDag dag;
+        GrammarScope scope(grammar);
         Recorded rec = record_has_match_engine(dag, len, pattern, lo, hi, engine);
         std::vector<int16_t> memo;
         std::memset(out, 0, sizeof *out);

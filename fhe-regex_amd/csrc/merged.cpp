@@ -108,6 +108,22 @@ class Merged {
                 for (size_t i = 1; i < re.cs.size(); ++i) r = OR(r, CMP(VNode::EQ, p, re.cs[i]));
                 return r;
             }
+            case Re::CLASS: {
+                int r = -1;
+                for (size_t i = 0; i + 1 < re.cs.size(); i += 2) {
+                    const uint8_t lo = re.cs[i], hi = re.cs[i + 1];
+                    int item;
+                    if (lo == hi) {
+                        item = CMP(VNode::EQ, p, lo);
+                    } else {
+                        const int ge = lo == 0 ? T_ : CMP(VNode::GT, p, (uint8_t)(lo - 1));
+                        const int le = hi == 255 ? T_ : CMP(VNode::LE, p, hi);
+                        item = AND(ge, le);
+                    }
+                    r = r < 0 ? item : OR(r, item);
+                }
+                return r;
+            }
             case Re::NOT: {
                 int c = char_cond(*re.a, p);
                 return c == -2 ? -2 : NOT(c);
@@ -123,6 +139,7 @@ class Merged {
             case Re::ANY:
             case Re::BETWEEN:
             case Re::RANGE:
+            case Re::CLASS:
             case Re::NOT: w = 1; return true;
             case Re::SEQ: {
                 size_t s = 0;
@@ -181,6 +198,7 @@ class Merged {
             case Re::ANY:
             case Re::BETWEEN:
             case Re::RANGE:
+            case Re::CLASS:
             case Re::NOT: {
                 for (size_t p = 0; p < L_; ++p) {
                     if (r[p] == ABSENT) continue;

@@ -38,6 +38,11 @@ std::string to_string(const Re& r) {
             for (size_t i = 0; i < r.xs.size(); ++i) o << (i ? "," : "") << to_string(*r.xs[i]);
             o << ")";
             break;
+        case Re::CLASS:
+            o << "Class(";
+            for (size_t i = 0; i + 1 < r.cs.size(); i += 2) o << (i ? "," : "") << (int)r.cs[i] << "-" << (int)r.cs[i + 1];
+            o << ")";
+            break;
     }
     return o.str();
 }
@@ -93,7 +98,8 @@ inline PR fail(bool committed) { PR r; r.committed = committed; return r; }
 
 struct Parser {
     const std::string& s;
-    explicit Parser(const std::string& str) : s(str) {}
+    const bool ext;  // FR_GRAMMAR_EXT
+    Parser(const std::string& str, bool e) : s(str), ext(e) {}
     bool at(size_t i, char ch) const { return i < s.size() && s[i] == ch; }
     static bool letter(unsigned char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
     static bool nonesc(unsigned char c) {  // parser.rs:252-254
@@ -172,11 +178,15 @@ struct Parser {
         if (at(i, '\\') && i + 1 < s.size()) return ok(mk_char((uint8_t)s[i + 1]), i + 2);
         if (i < s.size() && (letter((unsigned char)s[i]) || nonesc((unsigned char)s[i])))
             return ok(mk_char((uint8_t)s[i]), i + 1);
+        if (ext && is_digit(i)) return ok(mk_char((uint8_t)s[i]), i + 1);  // extension: bare digits
         if (at(i, '[')) {
             PR r = range(i + 1);
-            if (!r.ok) return fail(true);
-            if (!at(r.pos, ']')) return fail(true);
-            return ok(r.node, r.pos + 1);
+            if (r.ok && at(r.pos, ']')) return ok(r.node, r.pos + 1);
+            if (!ext) return fail(true);
+            // extension: attempt(reference class) failed -> general class
+            PR x = ext_class(i + 1);
+            if (!x.ok || !at(x.pos, ']')) return fail(true);
+            return ok(x.node, x.pos + 1);
         }
         if (at(i, '(')) {
             PR r = regex(i + 1);
@@ -211,6 +221,45 @@ struct Parser {
             return ok(q, j);
         }
         return fail(false);
+    }
+    // grammar extension: class := '^' class | item+ ; item := cc '-' cc | cc ;
+    // cc := letter | digit | '\\' byte | one of the 14 symbols except '-'
+    bool class_char(size_t i, uint8_t& c, size_t& next) const {
+        if (at(i, '\\') && i + 1 < s.size()) { c = (uint8_t)s[i + 1]; next = i + 2; return true; }
+        if (i < s.size() && (letter((unsigned char)s[i]) || is_digit(i) || (nonesc((unsigned char)s[i]) && s[i] != '-'))) {
+            c = (uint8_t)s[i];
+            next = i + 1;
+            return true;
+        }
+        return false;
+    }
+    PR ext_class(size_t i) {
+        if (at(i, '^')) {
+            PR r = ext_class(i + 1);
+            if (!r.ok) return fail(true);
+            auto q = std::make_shared<Re>();
+            q->kind = Re::NOT;
+            q->a = r.node;
+            return ok(q, r.pos);
+        }
+        auto q = std::make_shared<Re>();
+        q->kind = Re::CLASS;
+        size_t j = i;
+        uint8_t lo, hi;
+        size_t n1, n2;
+        while (class_char(j, lo, n1)) {
+            if (at(n1, '-') && class_char(n1 + 1, hi, n2)) {
+                if (hi < lo) throw Error(FR_ERR_PARSE, "character class range out of order");
+                j = n2;
+            } else {
+                hi = lo;
+                j = n1;
+            }
+            q->cs.push_back(lo);
+            q->cs.push_back(hi);
+        }
+        if (q->cs.empty()) return fail(j != i);
+        return ok(q, j);
     }
     // repeated (parser.rs:296-347); always called under attempt() by factor,
     // so only success or panic is observable.
@@ -264,8 +313,16 @@ struct Parser {
 };
 }  // namespace
 
-ReP parse(const std::string& pattern) {
-    Parser ps(pattern);
+static thread_local int g_grammar = FR_GRAMMAR_REFERENCE;
+int current_grammar() { return g_grammar; }
+GrammarScope::GrammarScope(int grammar) : prev_(g_grammar) { g_grammar = grammar; }
+GrammarScope::~GrammarScope() { g_grammar = prev_; }
+
+ReP parse(const std::string& pattern) { return parse(pattern, g_grammar); }
+
+ReP parse(const std::string& pattern, int grammar) {
+    if (grammar != FR_GRAMMAR_REFERENCE && grammar != FR_GRAMMAR_EXT) throw Error(FR_ERR_INVALID, "unknown grammar");
+    Parser ps(pattern, grammar == FR_GRAMMAR_EXT);
     const std::string& s = pattern;
     size_t i = 0;
     if (!ps.at(0, '/')) throw Error(FR_ERR_PARSE, "failed to parse regular expression");
@@ -511,6 +568,28 @@ std::vector<Branch> build_branches(size_t L, const ReP& re, size_t p) {
                          for (size_t i = 1; i < cs.size(); ++i) {
                              Val e = ex.ct_eq(ex.ct_pos(at), ex.ct_constant(cs[i]));
                              res = ex.ct_or(res, e);
+                         }
+                         return res;
+                     }),
+                     p + 1}};
+        }
+        case Re::CLASS: {  // grammar extension: OR over items of [lo <= c <= hi]
+            std::vector<uint8_t> cs = re->cs;
+            int at = (int)p;
+            return {{lazy([cs, at](Execution& ex) {
+                         Val res{};
+                         for (size_t i = 0; i + 1 < cs.size(); i += 2) {
+                             const uint8_t lo = cs[i], hi = cs[i + 1];
+                             Val item;
+                             if (lo == hi) {
+                                 item = ex.ct_eq(ex.ct_pos(at), ex.ct_constant(lo));
+                             } else {
+                                 // c >= lo as ct_ge(c, lo - 1): ct_ge is strict (execution.rs:93)
+                                 Val ge = lo == 0 ? ex.ct_true() : ex.ct_ge(ex.ct_pos(at), ex.ct_constant((uint8_t)(lo - 1)));
+                                 Val le = hi == 255 ? ex.ct_true() : ex.ct_le(ex.ct_pos(at), ex.ct_constant(hi));
+                                 item = ex.ct_and(ge, le);
+                             }
+                             res = i == 0 ? item : ex.ct_or(res, item);
                          }
                          return res;
                      }),

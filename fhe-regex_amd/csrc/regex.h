@@ -17,7 +17,9 @@ namespace fr {
 struct Re;
 using ReP = std::shared_ptr<const Re>;
 struct Re {
-    enum Kind { SOF, EOF_, ANY, CHAR, BETWEEN, RANGE, NOT, EITHER, OPTIONAL, REPEATED, SEQ } kind;
+    // CLASS (grammar extension, not in the reference): cs = lo0,hi0,lo1,hi1,...
+    // inclusive byte ranges; one character matches if it lies in any of them
+    enum Kind { SOF, EOF_, ANY, CHAR, BETWEEN, RANGE, NOT, EITHER, OPTIONAL, REPEATED, SEQ, CLASS } kind;
     uint8_t c = 0, from = 0, to = 0;
     std::vector<uint8_t> cs;
     ReP a, b;
@@ -29,7 +31,22 @@ struct Re {
 std::string to_string(const Re& r);
 // parse(pattern): parser.rs:146-185.  Throws Error(FR_ERR_PARSE) for the
 // reference's Err, Error(FR_ERR_REF_PANIC) where the reference panics.
+// grammar FR_GRAMMAR_EXT (beyond the reference) additionally accepts bare
+// digits as characters and bracket classes mixing letters, digits, escapes and
+// ranges ([a-z0-9], [^A-Z_]) — only where the reference grammar fails, so every
+// pattern the reference accepts parses to the same AST.  The default is the
+// calling thread's grammar (GrammarScope), initially FR_GRAMMAR_REFERENCE.
+ReP parse(const std::string& pattern, int grammar);
 ReP parse(const std::string& pattern);
+int current_grammar();
+struct GrammarScope {  // sets the thread's grammar for parse(pattern)
+    explicit GrammarScope(int grammar);
+    ~GrammarScope();
+    GrammarScope(const GrammarScope&) = delete;
+    GrammarScope& operator=(const GrammarScope&) = delete;
+  private:
+    int prev_;
+};
 
 // ------------------------------------------------------------ value DAG
 // What the reference actually computes homomorphically: one node per distinct

@@ -33,6 +33,7 @@ FR_OK = 0
 ERR_INVALID, ERR_PARSE, ERR_REF_PANIC, ERR_NO_DEVICE, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_NON_ASCII = range(-1, -9, -1)
 LOWER_FAITHFUL, LOWER_THRESHOLD = 0, 1
 ENGINE_AUTO, ENGINE_ENUMERATE, ENGINE_MERGED = 0, 1, 2
+GRAMMAR_REFERENCE, GRAMMAR_EXT = 0, 1
 NULL_CT = 0xFFFFFFFF
 
 
@@ -122,6 +123,10 @@ _SIGS = {
                                      C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_engine": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_set_grammar": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_parse_ex": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_size_t]),
+    "fr_plain_match_g": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
+                                   C.c_int32, C.POINTER(PlainResult)]),
     "fr_plain_match_ex": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
                                     C.POINTER(PlainResult)]),
     "fr_plain_match": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32,
@@ -187,22 +192,24 @@ def default_params(k: Optional[int] = None, N: Optional[int] = None, ring: Optio
     return p
 
 
-def parse(pattern: str) -> str:
+def parse(pattern: str, grammar: int = GRAMMAR_REFERENCE) -> str:
+    """Canonical AST string (parser.rs:146-185; GRAMMAR_EXT: the opt-in class extension)."""
     buf = C.create_string_buffer(1 << 16)
-    _check(lib().fr_parse(pattern.encode("latin-1"), buf, len(buf)))
+    _check(lib().fr_parse_ex(pattern.encode("latin-1"), grammar, buf, len(buf)))
     return buf.value.decode()
 
 
 def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESHOLD,
-                start_lo: int = 0, start_hi: Optional[int] = None, engine: int = ENGINE_ENUMERATE) -> PlainResult:
+                start_lo: int = 0, start_hi: Optional[int] = None, engine: int = ENGINE_ENUMERATE,
+                grammar: int = GRAMMAR_REFERENCE) -> PlainResult:
     """Host-only symbolic run: reference counters + plaintext result of the
     recorded circuit and of the lowered PBS program."""
     if isinstance(content, str):
         content = content.encode("latin-1")
     hi = len(content) if start_hi is None else start_hi
     r = PlainResult()
-    _check(lib().fr_plain_match_ex(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, engine,
-                                   C.byref(r)))
+    _check(lib().fr_plain_match_g(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, engine,
+                                  grammar, C.byref(r)))
     return r
 
 
@@ -256,6 +263,11 @@ class Context:
         """ENGINE_AUTO (default), ENGINE_ENUMERATE (the reference's variant
         enumeration) or ENGINE_MERGED (state merging; same decrypted result)."""
         _check(lib().fr_set_engine(self.h, engine))
+
+    def set_grammar(self, grammar: int):
+        """GRAMMAR_REFERENCE (default: parser.rs exactly) or GRAMMAR_EXT (also
+        bare digits and mixed bracket classes such as [a-z0-9]; beyond the reference)."""
+        _check(lib().fr_set_grammar(self.h, grammar))
 
     def set_multi_value(self, on: bool):
         _check(lib().fr_set_multi_value(self.h, int(on)))

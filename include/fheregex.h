@@ -199,6 +199,18 @@ int fr_plain_match(const char* content, size_t len, const char* pattern, size_t 
  *   logarithmic depth for fixed-width loops; ct_ops counts circuit operations.
  * FR_ENGINE_AUTO (default): enumerate within 2^22 variants, else merged. */
 enum { FR_ENGINE_AUTO = 0, FR_ENGINE_ENUMERATE = 1, FR_ENGINE_MERGED = 2 };
+/* Pattern grammar (fr_set_grammar, fr_parse_ex, fr_plain_match_g):
+ * FR_GRAMMAR_REFERENCE (default): parser.rs:146-351 exactly ([a-z0-9] is Err).
+ * FR_GRAMMAR_EXT (beyond the reference, opt-in): also bare digits as
+ *   characters and bracket classes mixing letters, digits, escapes and
+ *   inclusive ranges — [a-z0-9], [^A-Z_], [\-a] — tried only where the
+ *   reference grammar fails, so every pattern the reference accepts keeps its
+ *   AST (including [a-z]'s strict lower bound, engine.rs:99-111). */
+enum { FR_GRAMMAR_REFERENCE = 0, FR_GRAMMAR_EXT = 1 };
+int fr_set_grammar(fr_ctx* ctx, int32_t grammar);
+int fr_parse_ex(const char* pattern, int32_t grammar, char* buf, size_t buflen);
+int fr_plain_match_g(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
+                     int32_t lowering, int32_t engine, int32_t grammar, fr_plain_result* out);
 int fr_set_engine(fr_ctx* ctx, int32_t engine);
 int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                       int32_t lowering, int32_t engine, fr_plain_result* out);

@@ -19,6 +19,13 @@ the reference's *decrypted* result.  Keys are hash-consed into integer ids so
 that structural equality of ``Executed`` trees is id equality (the reference
 hashes whole trees; the counts are identical).
 
+Grammar extension (beyond the reference, ``ext=True``; mirrors the product's
+FR_GRAMMAR_EXT): bare digits are characters, and a bracket whose reference
+parse fails is re-read as a class of letters, digits, escapes and inclusive
+ranges (``Class(lo-hi,...)``).  Patterns the reference accepts keep their AST.
+Parity of the extension is against this restatement alone (the reference
+returns Err for these patterns).
+
 Reference panics (``parse_digits("")`` at parser.rs:349-351, ``Seq{[]}``
 indexing at engine.rs:189-190) are raised as ``ReferencePanic``.
 
@@ -84,6 +91,8 @@ class Node:
             return f"Repeated({self.a},{lo},{hi})"
         if k == "Seq":
             return "Seq(" + ",".join(str(x) for x in self.xs) + ")"
+        if k == "Class":
+            return "Class(" + ",".join(f"{self.cs[i]}-{self.cs[i + 1]}" for i in range(0, len(self.cs), 2)) + ")"
         raise ValueError(k)
 
 
@@ -257,14 +266,54 @@ def _factor():
     )
 
 
+_EXT = False  # grammar extension active (set by parse(..., ext=True))
+
+
+def _when_ext(q):
+    def p(s, i):
+        return q(s, i) if _EXT else (ERR, False)
+    return p
+
+
+def _bracket():
+    ref = _between(_byte(ord("[")), _byte(ord("]")), _lazy(_range))
+    ext = _between(_byte(ord("[")), _byte(ord("]")), _lazy(_ext_class))
+
+    def p(s, i):
+        if not _EXT:
+            return ref(s, i)
+        return _choice(_attempt(ref), ext)(s, i)
+    return p
+
+
 def _atom():
-    # parser.rs:256-269
+    # parser.rs:256-269 (+ the extension's bare digits and classes)
     return _choice(
         _map(_byte(ord(".")), lambda _: Node("Any")),
         _map(_attempt(_map(_seq(_byte(ord("\\")), _any), lambda v: v[1])), lambda c: Node("Char", c=c)),
         _map(_choice(_letter, _satisfy(lambda b: b in NON_ESCAPABLE)), lambda c: Node("Char", c=c)),
-        _between(_byte(ord("[")), _byte(ord("]")), _lazy(_range)),
+        _map(_when_ext(_digit), lambda c: Node("Char", c=c)),
+        _bracket(),
         _between(_byte(ord("(")), _byte(ord(")")), _lazy(_regex)),
+    )
+
+
+def _ext_class():
+    # extension: class := '^' class | item+ ; item := cc '-' cc | cc
+    cc = _choice(
+        _attempt(_map(_seq(_byte(ord("\\")), _any), lambda v: v[1])),
+        _satisfy(lambda b: (65 <= b <= 90) or (97 <= b <= 122) or (48 <= b <= 57)
+                 or (b in NON_ESCAPABLE and b != ord("-"))),
+    )
+
+    def rng(v):
+        if v[2] < v[0]:
+            raise ParseError("character class range out of order")
+        return (v[0], v[2])
+    item = _choice(_attempt(_map(_seq(cc, _byte(ord("-")), cc), rng)), _map(cc, lambda c: (c, c)))
+    return _choice(
+        _map(_seq(_byte(ord("^")), _lazy(_ext_class)), lambda v: Node("Not", a=v[1])),
+        _map(_many(item, min1=True), lambda its: Node("Class", cs=tuple(x for it in its for x in it))),
     )
 
 
@@ -302,8 +351,17 @@ def _repeated():
     )
 
 
-def parse(pattern: str | bytes) -> Node:
-    """parser.rs:146-185."""
+def parse(pattern: str | bytes, ext: bool = False) -> Node:
+    """parser.rs:146-185 (ext: the grammar extension, see the module docstring)."""
+    global _EXT
+    prev, _EXT = _EXT, bool(ext)
+    try:
+        return _parse(pattern)
+    finally:
+        _EXT = prev
+
+
+def _parse(pattern: str | bytes) -> Node:
     s = pattern.encode() if isinstance(pattern, str) else bytes(pattern)
 
     def wrap(v):
@@ -474,6 +532,22 @@ def build_branches(L: int, re: Node, p: int) -> List[Tuple[Lazy, int]]:
                 res = ex.ct_or(res, e)
             return res
         return [(rng, p + 1)]
+    if k == "Class":  # extension: OR over items of [lo <= c <= hi]
+        cs = re.cs
+
+        def cls(ex, p=p, cs=cs):
+            res = None
+            for i in range(0, len(cs), 2):
+                lo, hi = cs[i], cs[i + 1]
+                if lo == hi:
+                    item = ex.ct_eq(ex.ct_pos(p), ex.ct_constant(lo))
+                else:  # c >= lo as ct_ge(c, lo - 1): ct_ge is strict (execution.rs:93)
+                    ge = ex.ct_true() if lo == 0 else ex.ct_ge(ex.ct_pos(p), ex.ct_constant(lo - 1))
+                    le = ex.ct_true() if hi == 255 else ex.ct_le(ex.ct_pos(p), ex.ct_constant(hi))
+                    item = ex.ct_and(ge, le)
+                res = item if res is None else ex.ct_or(res, item)
+            return res
+        return [(cls, p + 1)]
     if k == "Repeated":
         at_least = 0 if re.lo is None else re.lo
         at_most = (L - p) if re.hi is None else re.hi
@@ -512,12 +586,13 @@ class MatchResult:
     n_branches: int
 
 
-def has_match(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None) -> MatchResult:
+def has_match(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None,
+              ext: bool = False) -> MatchResult:
     """engine.rs:8-42.  ``start_lo/start_hi`` restrict the start offsets (the
     multi-GPU shard of §8(e)); the defaults reproduce the reference."""
     if isinstance(content, str):
         content = content.encode()
-    re = parse(pattern)
+    re = parse(pattern, ext)
     L = len(content)
     hi = L if start_hi is None else start_hi
     branches = []
@@ -553,6 +628,8 @@ def _char_ok(re: Node, ch: int) -> bool:
         return ch > re.f and ch <= re.t
     if k == "Range":
         return ch in re.cs
+    if k == "Class":
+        return any(re.cs[i] <= ch <= re.cs[i + 1] for i in range(0, len(re.cs), 2))
     if k == "Not":
         return not _char_ok(re.a, ch)
     raise ValueError("Not over a multi-branch operand")
@@ -572,7 +649,7 @@ def _reach(L: int, content: bytes, re: Node, S: dict) -> dict:
     def put(q, v):
         out[q] = out.get(q, False) or v
 
-    if k in ("Char", "Any", "Between", "Range", "Not"):
+    if k in ("Char", "Any", "Between", "Range", "Class", "Not"):
         for p, v in S.items():
             put(p + 1, v and _char_ok(re, content[p]))
         return out
@@ -618,11 +695,12 @@ def _reach(L: int, content: bytes, re: Node, S: dict) -> dict:
     raise ReferencePanic("unmatched regex variant")
 
 
-def has_match_reach(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None) -> int:
+def has_match_reach(content: bytes | str, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None,
+                    ext: bool = False) -> int:
     """Plaintext result of has_match by position-set simulation (polynomial)."""
     if isinstance(content, str):
         content = content.encode()
-    re = parse(pattern)
+    re = parse(pattern, ext)
     L = len(content)
     hi = L if start_hi is None else min(start_hi, L)
     out = _reach(L, content, re, {p: True for p in range(start_lo, hi)})

@@ -6,7 +6,25 @@ LETTERS = "abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ"
 SYMS = "&;:,`~-_!@#%'\""
 
 
-def rand_atom(rng, depth):
+def rand_ext_class(rng):
+    """A bracket class of the grammar extension (FR_GRAMMAR_EXT)."""
+    items = []
+    for _ in range(rng.randint(1, 3)):
+        k = rng.random()
+        if k < 0.4:
+            a, b = sorted(rng.sample("0123456789", 2))
+        elif k < 0.7:
+            a, b = sorted(rng.sample("abcdexyz", 2))
+        else:
+            a = b = rng.choice("0159aAz_\\-")
+        items.append(a if a == b else f"{a}-{b}")
+    body = "".join("\\-" if it == "-" else ("\\\\" if it == "\\" else it) for it in items)
+    return "[" + ("^" if rng.random() < 0.3 else "") + body + "]"
+
+
+def rand_atom(rng, depth, ext=False):
+    if ext and rng.random() < 0.3:
+        return rng.choice("0123") if rng.random() < 0.3 else rand_ext_class(rng)
     r = rng.random()
     if r < 0.45:
         return rng.choice("abcdeABC")
@@ -28,12 +46,12 @@ def rand_atom(rng, depth):
             return f"[^{a}-{b}]"
         return "[^" + "".join(rng.sample("abcxyz", rng.randint(1, 3))) + "]"
     if depth < 2:
-        return "(" + rand_regex(rng, depth + 1) + ")"
+        return "(" + rand_regex(rng, depth + 1, ext) + ")"
     return rng.choice("abc")
 
 
-def rand_factor(rng, depth):
-    a = rand_atom(rng, depth)
+def rand_factor(rng, depth, ext=False):
+    a = rand_atom(rng, depth, ext)
     r = rng.random()
     if r < 0.6:
         return a
@@ -50,19 +68,19 @@ def rand_factor(rng, depth):
     return a + "{%s,%s}" % (lo, hi)
 
 
-def rand_term(rng, depth):
-    return "".join(rand_factor(rng, depth) for _ in range(rng.randint(1, 3)))
+def rand_term(rng, depth, ext=False):
+    return "".join(rand_factor(rng, depth, ext) for _ in range(rng.randint(1, 3)))
 
 
-def rand_regex(rng, depth=0):
-    t = rand_term(rng, depth)
+def rand_regex(rng, depth=0, ext=False):
+    t = rand_term(rng, depth, ext)
     if rng.random() < 0.25:
-        t += "|" + rand_term(rng, depth)
+        t += "|" + rand_term(rng, depth, ext)
     return t
 
 
-def rand_pattern(rng):
-    p = "/" + ("^" if rng.random() < 0.25 else "") + rand_regex(rng) + ("$" if rng.random() < 0.25 else "") + "/"
+def rand_pattern(rng, ext=False):
+    p = "/" + ("^" if rng.random() < 0.25 else "") + rand_regex(rng, 0, ext) + ("$" if rng.random() < 0.25 else "") + "/"
     if rng.random() < 0.2:
         p += "i"
     return p

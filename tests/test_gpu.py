@@ -290,6 +290,26 @@ def test_config5_512_merged(gctx):
         gctx.set_engine(F.ENGINE_AUTO)
 
 
+def test_config3_as_written_256(gctx):
+    """BASELINE config 3, /^[a-z0-9]+$/ on 256 encrypted chars, under the
+    opt-in grammar extension (the reference returns Err): positive content and
+    negatives one character outside a range, vs the oracle's extension."""
+    import random
+    from test_grammar_ext import CONFIG3, config3_contents
+    pos, negs = config3_contents(random.Random(3))
+    with pytest.raises(F.ParseError):
+        _config(gctx, pos[:8], CONFIG3, 13)
+    gctx.set_grammar(F.GRAMMAR_EXT)
+    try:
+        for i, s in enumerate([pos, negs[0], negs[4]]):
+            got, st = _config(gctx, s, CONFIG3, 14 + i)
+            exp = ro.has_match(s, CONFIG3, ext=True)
+            assert got == exp.result == (1 if s == pos else 0), i
+            assert (st.ct_ops, st.cache_hits) == (exp.ct_ops, exp.cache_hits)
+    finally:
+        gctx.set_grammar(F.GRAMMAR_REFERENCE)
+
+
 def test_faithful_lowering(gctx):
     rng = np.random.default_rng(8)
     s = _printable(rng, 64)
