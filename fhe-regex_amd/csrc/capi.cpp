@@ -75,6 +75,8 @@ struct fr_ctx {
     int lowering = FR_LOWER_THRESHOLD;
     int engine = FR_ENGINE_AUTO;
     int grammar = FR_GRAMMAR_REFERENCE;
+    int keygen = FR_KEYGEN_AUTO;
+    bool sk_on_device = false;  // server key generated on the device (export downloads it)
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
 
     Device& device() {
@@ -396,6 +398,13 @@ int fr_set_engine(fr_ctx* ctx, int32_t engine) {
     })
 }
 
+int fr_set_keygen(fr_ctx* ctx, int32_t where) {
+    FR_TRY({
+        NEED(ctx && where >= FR_KEYGEN_AUTO && where <= FR_KEYGEN_DEVICE);
+        ctx->keygen = where;
+    })
+}
+
 int fr_set_grammar(fr_ctx* ctx, int32_t grammar) {
     FR_TRY({
         NEED(ctx && (grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT));
@@ -449,9 +458,20 @@ int fr_gen_server_key(fr_ctx* ctx, uint64_t seed) {
     FR_TRY({
         NEED(ctx);
         if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
-        gen_ksk(ctx->p, ctx->ck, seed, ctx->ksk);
-        gen_bsk(ctx->p, ctx->ck, seed, ctx->bsk);
-        if (ctx->dev) ctx->dev->upload_keys(ctx->ksk, ctx->bsk);
+        const bool on_dev = ctx->dev && ctx->p.ring == FR_RING_FFT && ctx->keygen != FR_KEYGEN_HOST;
+        if (ctx->keygen == FR_KEYGEN_DEVICE && !on_dev)
+            throw Error(ctx->dev ? FR_ERR_INVALID : FR_ERR_NO_DEVICE, "device keygen needs a device and the FFT ring");
+        ctx->has_sk = false;
+        if (on_dev) {
+            ctx->ksk.clear();
+            ctx->bsk.clear();
+            ctx->dev->gen_server_key(ctx->ck, seed);
+        } else {
+            gen_ksk(ctx->p, ctx->ck, seed, ctx->ksk);
+            gen_bsk(ctx->p, ctx->ck, seed, ctx->bsk);
+            if (ctx->dev) ctx->dev->upload_keys(ctx->ksk, ctx->bsk);
+        }
+        ctx->sk_on_device = on_dev;
         ctx->has_sk = true;
     })
 }
@@ -469,6 +489,10 @@ int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* b
     FR_TRY({
         NEED(ctx);
         if (!ctx->has_sk) throw Error(FR_ERR_NO_KEY, "server key not generated");
+        if (ctx->sk_on_device) {
+            ctx->device().download_server_key(ksk, ksk_len, bsk, bsk_len);
+            return FR_OK;
+        }
         if (ksk) {
             NEED(ksk_len == ctx->ksk.size());
             std::memcpy(ksk, ctx->ksk.data(), 8 * ksk_len);

@@ -36,6 +36,8 @@ struct DeviceTimers {
     uint64_t br_launches = 0, br_gates = 0, lut_outputs = 0;
 };
 
+struct ClientKey;
+
 class Device {
   public:
     Device(const Params& p, int device);
@@ -49,6 +51,11 @@ class Device {
     // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod Q [i][r][c][coef]
     void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
     bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk_); }
+    // server-key generation on the device (keygen.hip; FFT ring): the same keys
+    // as gen_ksk + gen_bsk on the host, bit for bit; the torus keys stay on the
+    // device for download_server_key
+    void gen_server_key(const ClientKey& ck, uint64_t seed);
+    void download_server_key(uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
 
     // arena of big-LWE slots
     int alloc_slot();
@@ -88,6 +95,7 @@ class Device {
     void upload_fft_bsk(const std::vector<uint64_t>& bsk);
     void launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream);
     void free_fft();
+    void build_ksk_limbs();  // d_kl_ from d_ksk_
 
     Params p_;
     int dev_;
@@ -96,6 +104,7 @@ class Device {
     size_t small_batch_ = 256;
     void* stream_ = nullptr;  // hipStream_t
     uint64_t* d_ksk_ = nullptr;
+    uint64_t* d_tbsk_ = nullptr;  // torus BSK of a device-generated key (export)
     int8_t* d_kl_ = nullptr;      // KSK as balanced byte limbs [col*8 + limb][k] (MFMA keyswitch)
     int kl_cols_ = 0;
     bool ks_mfma_ = true;         // FR_KS_MFMA=0: the VALU lincomb+keyswitch kernel

@@ -972,6 +972,7 @@ Device::~Device() {
     (void)hipSetDevice(dev_);
     if (stream_) (void)hipStreamSynchronize(STREAM);
     (void)hipFree(d_ksk_);
+    (void)hipFree(d_tbsk_);
     (void)hipFree(d_kl_);
     (void)hipFree(d_dig_);
     (void)hipFree(d_bsk_);
@@ -1063,6 +1064,20 @@ void Device::zero_slot(int slot) {
     HIP_CHECK(hipMemsetAsync(d_arena_ + (size_t)slot * p_.slot_stride(), 0, 8 * (size_t)p_.lwe_len(), STREAM));
 }
 
+// byte-limb form of the KSK for the MFMA keyswitch
+void Device::build_ksk_limbs() {
+    const int KD = p_.big() * p_.ks_level, ncols = p_.n + 1;
+    const int nlc = ((ncols * 8 + 127) / 128) * 128;  // whole 4-wave column groups
+    (void)hipFree(d_kl_);
+    d_kl_ = nullptr;
+    HIP_CHECK(hipMalloc(&d_kl_, (size_t)nlc * KD));
+    HIP_CHECK(hipMemsetAsync(d_kl_, 0, (size_t)nlc * KD, STREAM));
+    k_ksk_limbs<<<dim3((unsigned)((KD + 255) / 256), (unsigned)(nlc / 8)), 256, 0, STREAM>>>(d_ksk_, KD, ncols, nlc,
+                                                                                          d_kl_);
+    HIP_CHECK(hipGetLastError());
+    kl_cols_ = nlc;
+}
+
 void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk) {
     if (ksk.size() != (size_t)p_.big() * p_.ks_level * (p_.n + 1)) throw Error(FR_ERR_INVALID, "ksk size");
     if (bsk.size() != p_.bsk_len()) throw Error(FR_ERR_INVALID, "bsk size");
@@ -1072,19 +1087,9 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
     d_bsk_ = nullptr;
     HIP_CHECK(hipMalloc(&d_ksk_, 8 * ksk.size()));
     HIP_CHECK(hipMemcpy(d_ksk_, ksk.data(), 8 * ksk.size(), hipMemcpyHostToDevice));
-    {
-        // byte-limb form of the KSK for the MFMA keyswitch
-        const int KD = p_.big() * p_.ks_level, ncols = p_.n + 1;
-        const int nlc = ((ncols * 8 + 127) / 128) * 128;  // whole 4-wave column groups
-        (void)hipFree(d_kl_);
-        d_kl_ = nullptr;
-        HIP_CHECK(hipMalloc(&d_kl_, (size_t)nlc * KD));
-        HIP_CHECK(hipMemsetAsync(d_kl_, 0, (size_t)nlc * KD, STREAM));
-        k_ksk_limbs<<<dim3((unsigned)((KD + 255) / 256), (unsigned)(nlc / 8)), 256, 0, STREAM>>>(d_ksk_, KD, ncols, nlc,
-                                                                                              d_kl_);
-        HIP_CHECK(hipGetLastError());
-        kl_cols_ = nlc;
-    }
+    (void)hipFree(d_tbsk_);  // host-generated keys: export reads the host copy
+    d_tbsk_ = nullptr;
+    build_ksk_limbs();
     if (p_.ring == FR_RING_FFT) {
         upload_fft_bsk(bsk);
         return;

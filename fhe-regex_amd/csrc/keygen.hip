@@ -1,0 +1,266 @@
+// Server-key generation on the device (the reference's
+// ServerKey::new at src/regex/engine.rs:252 and gen_keys_radix at
+// src/regex/ciphertext.rs:44).  Bit-identical to keys.cpp's gen_ksk +
+// gen_bsk_torus followed by fft::bsk_to_fourier (and therefore to the oracle's
+// keygen): the same ChaCha20 words (chacha.h) for every mask, exact mod-2^64
+// sums for the bodies, the same host Box-Muller noise (uploaded), and the same
+// butterfly sequence for the Fourier transform.
+//
+// Kernels (all integer / f64 add-and-multiply work, HBM-bound or LDS-bound):
+//   k_gen_ksk      one wave per KSK row (kN * ks_level rows): masks from ChaCha
+//                  blocks, <mask, s_small> reduced over the wave, + s_big[i] *
+//                  2^(64 - B(j+1)) + noise
+//   k_gen_bsk      one workgroup per GGSW row (w, r): masks A_j from ChaCha into
+//                  LDS, body = sum_j A_j * S_j (negacyclic, binary S: one
+//                  add/sub per set bit of S per coefficient) + noise, gadget m_w
+//                  2^(64 - pbs_base_log) on coefficient 0 of component r
+//   k_bsk_fourier  one workgroup per polynomial: fold, forward negacyclic FFT in
+//                  LDS (fft.h butterflies, host twiddles), scale 2^-log2(M),
+//                  written in both lane layouts of the blind-rotation kernels
+#include <hip/hip_runtime.h>
+
+#include <cstring>
+#include <vector>
+
+#include "chacha.h"
+#include "device.h"
+#include "fft.h"
+#include "geo.h"
+#include "keys.h"
+
+namespace fr {
+
+#define KG_CHECK(x)                                                                          \
+    do {                                                                                     \
+        hipError_t _e = (x);                                                                 \
+        if (_e != hipSuccess)                                                                \
+            throw Error(FR_ERR_HIP, std::string("HIP error (keygen): ") + hipGetErrorString(_e)); \
+    } while (0)
+
+// u64 number 8*blk + q of a ChaCha stream: words (2q, 2q+1) of block blk
+__device__ __forceinline__ uint64_t chacha_u64(const uint32_t* w, int q) {
+    return (uint64_t)w[2 * q] | ((uint64_t)w[2 * q + 1] << 32);
+}
+
+// ksk[row][t], row = i * L + j; masks are u64 numbers row * n + t of STREAM_KSK_MASK
+__global__ void __launch_bounds__(64) k_gen_ksk(uint64_t seed, int n, int L, int B, const uint64_t* __restrict__ s_small,
+                                                const uint64_t* __restrict__ s_big, const int64_t* __restrict__ noise,
+                                                uint64_t* __restrict__ ksk) {
+    const int row = blockIdx.x, lane = threadIdx.x;
+    const int i = row / L, j = row % L;
+    const uint64_t first = (uint64_t)row * n, last = first + n;
+    uint64_t* o = ksk + (size_t)row * (n + 1);
+    uint64_t acc = 0;
+    for (uint64_t b = (first >> 3) + lane; b <= ((last - 1) >> 3); b += 64) {
+        uint32_t w[16];
+        chacha_block(seed, STREAM_KSK_MASK, b, w);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const uint64_t idx = b * 8 + q;
+            if (idx >= first && idx < last) {
+                const int t = (int)(idx - first);
+                const uint64_t v = chacha_u64(w, q);
+                o[t] = v;
+                acc += v * s_small[t];
+            }
+        }
+    }
+    // wave sum mod 2^64 (order-free)
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) o[n] = acc + (s_big[i] << (64 - B * (j + 1))) + (uint64_t)noise[row];
+}
+
+// one GGSW row (w, r) of the torus BSK [w][r][c][coef]; 256 threads, N / 256
+// coefficients per thread; LDS: the mask polynomial A_j (N u64)
+template <int N>
+__global__ void __launch_bounds__(256) k_gen_bsk(uint64_t seed, int k, const uint64_t* __restrict__ s_big,
+                                                 const uint8_t* __restrict__ msg, const int32_t* __restrict__ noise,
+                                                 uint64_t gadget, uint64_t* __restrict__ bsk) {
+    constexpr int PER = N / 256;
+    __shared__ uint64_t A[N];
+    __shared__ uint32_t sbits[N / 32];
+    const int kp1 = k + 1, tid = threadIdx.x;
+    const int w = blockIdx.x / kp1, r = blockIdx.x % kp1;
+    uint64_t* row = bsk + ((size_t)w * kp1 + r) * kp1 * N;
+    uint64_t acc[PER];
+#pragma unroll
+    for (int q = 0; q < PER; ++q) acc[q] = 0;
+    for (int j = 0; j < k; ++j) {
+        const uint64_t base = (((uint64_t)w * kp1 + r) * k + j) * N;  // N % 8 == 0: whole ChaCha blocks
+        for (int b = tid; b < N / 8; b += 256) {
+            uint32_t wd[16];
+            chacha_block(seed, STREAM_BSK_MASK, (base >> 3) + b, wd);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                uint64_t v = chacha_u64(wd, q);
+                A[8 * b + q] = v;
+                // the gadget lands on coefficient 0 of component r after the body used A
+                if (j == r && b == 0 && q == 0 && msg[w]) v += gadget;
+                row[(size_t)j * N + 8 * b + q] = v;
+            }
+        }
+        const uint64_t* S = s_big + (size_t)j * N;
+        for (int x = tid; x < N / 32; x += 256) {
+            uint32_t m = 0;
+            for (int y = 0; y < 32; ++y) m |= (uint32_t)(S[32 * x + y] & 1) << y;
+            sbits[x] = m;
+        }
+        __syncthreads();
+        // body += X^u A for every set bit u of S_j: coefficient t gets A[t - u]
+        // (t >= u) or -A[t - u + N] (wrapped)
+        for (int x = 0; x < N / 32; ++x) {
+            uint32_t m = sbits[x];
+            while (m) {
+                const int u = 32 * x + __builtin_ctz(m);
+                m &= m - 1;
+#pragma unroll
+                for (int q = 0; q < PER; ++q) {
+                    const int t = tid + 256 * q;
+                    const int d = t - u;
+                    const uint64_t a = A[d >= 0 ? d : d + N];
+                    acc[q] = d >= 0 ? acc[q] + a : acc[q] - a;
+                }
+            }
+        }
+        __syncthreads();
+    }
+    const int32_t* e = noise + ((size_t)w * kp1 + r) * N;
+#pragma unroll
+    for (int q = 0; q < PER; ++q) {
+        const int t = tid + 256 * q;
+        uint64_t v = acc[q] + (uint64_t)(int64_t)e[t];
+        if (r == k && t == 0 && msg[w]) v += gadget;
+        row[(size_t)k * N + t] = v;
+    }
+}
+
+// fold + forward FFT + 1/M of one polynomial, written in the lane layouts of
+// the E = 8 and E = 4 kernels ([poly][m][lane], slot of (lane, m) per geo.h)
+template <int N>
+__global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict__ bsk, const double2* __restrict__ tw,
+                                                     int L8, int L4, double2* __restrict__ out8,
+                                                     double2* __restrict__ out4) {
+    constexpr int M = N / 2;
+    constexpr int LOG = __builtin_ctz(M);
+    __shared__ double2 z[M];
+    const int tid = threadIdx.x;
+    const size_t p = blockIdx.x;
+    const uint64_t* a = bsk + p * N;
+    for (int i = tid; i < M; i += 256) z[i] = make_double2((double)(int64_t)a[i], (double)(int64_t)a[i + M]);
+    __syncthreads();
+    for (int s = 0; s < LOG; ++s) {
+        const int h = M >> (s + 1);
+        for (int bi = tid; bi < M / 2; bi += 256) {
+            const int b = bi / h, j = b * 2 * h + bi % h;
+            const double2 c = tw[(1 << s) + b];
+            double2 lo = z[j], hi = z[j + h];
+            fft::fwd_bf(lo.x, lo.y, hi.x, hi.y, c.x, c.y);
+            z[j] = lo;
+            z[j + h] = hi;
+        }
+        __syncthreads();
+    }
+    const double scale = 1.0 / (double)M;  // 2^-LOG, exact
+    for (int idx = tid; idx < M; idx += 256) {
+        {  // E = 8
+            constexpr int E = 8, e = 3, T = M / E;
+            const int m = idx / T, tl = idx % T;
+            const int slot = (((tl >> L8) << (L8 + e)) | (tl & ((1 << L8) - 1))) + (m << L8);
+            const double2 v = z[slot];
+            out8[p * M + idx] = make_double2(v.x * scale, v.y * scale);
+        }
+        {  // E = 4
+            constexpr int E = 4, e = 2, T = M / E;
+            const int m = idx / T, tl = idx % T;
+            const int slot = (((tl >> L4) << (L4 + e)) | (tl & ((1 << L4) - 1))) + (m << L4);
+            const double2 v = z[slot];
+            out4[p * M + idx] = make_double2(v.x * scale, v.y * scale);
+        }
+    }
+}
+
+void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
+    if (p_.ring != FR_RING_FFT || p_.N != 2048 || p_.k != 1)
+        throw Error(FR_ERR_INVALID, "device keygen: FFT ring (k = 1, N = 2048) only");
+    const int N = p_.N, M = N / 2, kp1 = p_.k + 1, n = p_.n, L = p_.ks_level;
+    const size_t rows = (size_t)p_.big() * L, nw = p_.bsk_ggsw();
+    const size_t bsk_polys = nw * kp1 * kp1;
+    // host: the noise draws and per-GGSW messages
+    std::vector<int64_t> ksk_noise;
+    std::vector<int32_t> bsk_noise;
+    gen_ksk_noise(p_, seed, ksk_noise);
+    gen_bsk_noise_torus(p_, seed, bsk_noise);
+    const std::vector<uint8_t> msg = ggsw_messages(p_, ck);
+
+    uint64_t *d_ss = nullptr, *d_sb = nullptr;
+    int64_t* d_kn = nullptr;
+    int32_t* d_bn = nullptr;
+    uint8_t* d_msg = nullptr;
+    auto cleanup = [&] {
+        (void)hipFree(d_ss);
+        (void)hipFree(d_sb);
+        (void)hipFree(d_kn);
+        (void)hipFree(d_bn);
+        (void)hipFree(d_msg);
+    };
+    try {
+        const hipStream_t s = (hipStream_t)stream_;
+        KG_CHECK(hipMalloc(&d_ss, 8 * ck.s_small.size()));
+        KG_CHECK(hipMalloc(&d_sb, 8 * ck.s_big.size()));
+        KG_CHECK(hipMalloc(&d_kn, 8 * ksk_noise.size()));
+        KG_CHECK(hipMalloc(&d_bn, 4 * bsk_noise.size()));
+        KG_CHECK(hipMalloc(&d_msg, msg.size()));
+        KG_CHECK(hipMemcpyAsync(d_ss, ck.s_small.data(), 8 * ck.s_small.size(), hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_sb, ck.s_big.data(), 8 * ck.s_big.size(), hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_kn, ksk_noise.data(), 8 * ksk_noise.size(), hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_bn, bsk_noise.data(), 4 * bsk_noise.size(), hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_msg, msg.data(), msg.size(), hipMemcpyHostToDevice, s));
+
+        // KSK (torus) and its byte limbs
+        (void)hipFree(d_ksk_);
+        d_ksk_ = nullptr;
+        KG_CHECK(hipMalloc(&d_ksk_, 8 * rows * (n + 1)));
+        k_gen_ksk<<<(unsigned)rows, 64, 0, s>>>(seed, n, L, p_.ks_base_log, d_ss, d_sb, d_kn, d_ksk_);
+        KG_CHECK(hipGetLastError());
+        build_ksk_limbs();
+
+        // torus BSK, kept for export
+        (void)hipFree(d_tbsk_);
+        d_tbsk_ = nullptr;
+        KG_CHECK(hipMalloc(&d_tbsk_, 8 * p_.bsk_len()));
+        const uint64_t gadget = 1ULL << (64 - p_.pbs_base_log);
+        k_gen_bsk<2048><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
+        KG_CHECK(hipGetLastError());
+
+        // Fourier BSK in both lane layouts
+        for (double** dst : {&d_fbsk_, &d_fbsk4_}) {
+            (void)hipFree(*dst);
+            *dst = nullptr;
+            KG_CHECK(hipMalloc(dst, 16 * bsk_polys * M));
+        }
+        const int LOG = __builtin_ctz(M);
+        const int L8 = geo_lo(LOG, 3, (LOG + 2) / 3 - 1), L4 = geo_lo(LOG, 2, (LOG + 1) / 2 - 1);
+        k_bsk_fourier<2048><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
+                                                                (double2*)d_fbsk_, (double2*)d_fbsk4_);
+        KG_CHECK(hipGetLastError());
+        KG_CHECK(hipStreamSynchronize(s));
+    } catch (...) {
+        cleanup();
+        throw;
+    }
+    cleanup();
+}
+
+void Device::download_server_key(uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len) {
+    if (!d_ksk_ || !d_tbsk_) throw Error(FR_ERR_NO_KEY, "no device-generated server key");
+    if (ksk) {
+        if (ksk_len != (size_t)p_.big() * p_.ks_level * (p_.n + 1)) throw Error(FR_ERR_INVALID, "ksk size");
+        KG_CHECK(hipMemcpy(ksk, d_ksk_, 8 * ksk_len, hipMemcpyDeviceToHost));
+    }
+    if (bsk) {
+        if (bsk_len != p_.bsk_len()) throw Error(FR_ERR_INVALID, "bsk size");
+        KG_CHECK(hipMemcpy(bsk, d_tbsk_, 8 * bsk_len, hipMemcpyDeviceToHost));
+    }
+}
+
+}  // namespace fr

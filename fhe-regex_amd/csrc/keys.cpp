@@ -6,39 +6,18 @@
 // The GGSW ring is Z_Q[X]/(X^N+1), Q = p0*p1 in RNS form (rns.h).
 #include "keys.h"
 
+#include "chacha.h"
 #include "rns.h"
 
+#include <atomic>
+#include <climits>
 #include <cmath>
 #include <cstring>
 #include <thread>
 
 namespace fr {
 
-// ---------------------------------------------------------------- ChaCha20
-static inline uint32_t rotl32(uint32_t a, int b) { return (a << b) | (a >> (32 - b)); }
-#define FR_QR(a, b, c, d)                      \
-    a += b; d ^= a; d = rotl32(d, 16);         \
-    c += d; b ^= c; b = rotl32(b, 12);         \
-    a += b; d ^= a; d = rotl32(d, 8);          \
-    c += d; b ^= c; b = rotl32(b, 7);
-
-static void chacha_block(uint64_t seed, uint64_t stream, uint64_t counter, uint32_t out[16]) {
-    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                             (uint32_t)seed, (uint32_t)(seed >> 32), 0x243F6A88u, 0x85A308D3u,
-                             0x13198A2Eu, 0x03707344u, 0xA4093822u, 0x299F31D0u,
-                             (uint32_t)counter, (uint32_t)(counter >> 32), (uint32_t)stream,
-                             (uint32_t)(stream >> 32)};
-    uint32_t x[16];
-    std::memcpy(x, in, sizeof x);
-    for (int i = 0; i < 10; ++i) {
-        FR_QR(x[0], x[4], x[8], x[12]); FR_QR(x[1], x[5], x[9], x[13]);
-        FR_QR(x[2], x[6], x[10], x[14]); FR_QR(x[3], x[7], x[11], x[15]);
-        FR_QR(x[0], x[5], x[10], x[15]); FR_QR(x[1], x[6], x[11], x[12]);
-        FR_QR(x[2], x[7], x[8], x[13]); FR_QR(x[3], x[4], x[9], x[14]);
-    }
-    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
-}
-
+// ChaCha20: chacha.h (shared with the device key generator)
 uint64_t Rng::u64(uint64_t idx) {
     uint64_t blk = idx >> 3;
     if (!valid_ || blk != blk_) {
@@ -277,6 +256,35 @@ static void gen_bsk_torus(const Params& p, const ClientKey& ck, uint64_t seed, s
             if (msg) row[r * N] += gadget;
         }
     });
+}
+
+// noise terms of the device key generator (keygen.hip): the same draws as
+// gen_ksk / gen_bsk_torus above (Box-Muller stays on the host, where libm is
+// the reference for the bits)
+void gen_ksk_noise(const Params& p, uint64_t seed, std::vector<int64_t>& e) {
+    const size_t rows = (size_t)p.big() * p.ks_level;
+    e.resize(rows);
+    Rng rn(seed, STREAM_KSK_NOISE);
+    for (size_t row = 0; row < rows; ++row) e[row] = rn.gaussian(row, p.lwe_sigma);
+}
+void gen_bsk_noise_torus(const Params& p, uint64_t seed, std::vector<int32_t>& e) {
+    const size_t polys = p.bsk_ggsw() * (size_t)(p.k + 1), N = (size_t)p.N;
+    e.resize(polys * N);
+    std::atomic<bool> ok{true};
+    parallel_for((int)polys, [&](int q) {
+        Rng rn(seed, STREAM_BSK_NOISE);
+        for (size_t t = 0; t < N; ++t) {
+            const int64_t v = rn.gaussian((uint64_t)q * N + t, p.glwe_sigma);
+            if (v < INT32_MIN || v > INT32_MAX) ok = false;
+            e[(size_t)q * N + t] = (int32_t)v;
+        }
+    });
+    if (!ok) throw Error(FR_ERR_INVALID, "GLWE noise outside int32 (sigma too large for the device key generator)");
+}
+std::vector<uint8_t> ggsw_messages(const Params& p, const ClientKey& ck) {
+    std::vector<uint8_t> m(p.bsk_ggsw());
+    for (size_t w = 0; w < m.size(); ++w) m[w] = (uint8_t)ggsw_msg(p, ck, w);
+    return m;
 }
 
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk) {

@@ -52,6 +52,13 @@ void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
 // BSK: [GGSW w][row r in k+1][component c in k+1][coef], coefficient domain mod Q (rns.h);
 // GGSW w per Params::bsk_unroll (k = 1: 3 per pair of LWE coefficients).
 void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& bsk);
+// Host parts of the device key generator (Device::gen_server_key): the
+// Box-Muller noise of every KSK row (lwe sigma, torus units), of every BSK
+// body coefficient ([w][r][coef], glwe sigma, torus units) and the message bit
+// of every GGSW.
+void gen_ksk_noise(const Params& p, uint64_t seed, std::vector<int64_t>& e);
+void gen_bsk_noise_torus(const Params& p, uint64_t seed, std::vector<int32_t>& e);
+std::vector<uint8_t> ggsw_messages(const Params& p, const ClientKey& ck);
 
 // Fresh LWE encryptions of block messages (Delta = 2^59) under the big key.
 void encrypt_blocks(const Params& p, const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed,

@@ -34,6 +34,7 @@ ERR_INVALID, ERR_PARSE, ERR_REF_PANIC, ERR_NO_DEVICE, ERR_HIP, ERR_NO_KEY, ERR_O
 LOWER_FAITHFUL, LOWER_THRESHOLD = 0, 1
 ENGINE_AUTO, ENGINE_ENUMERATE, ENGINE_MERGED = 0, 1, 2
 GRAMMAR_REFERENCE, GRAMMAR_EXT = 0, 1
+KEYGEN_AUTO, KEYGEN_HOST, KEYGEN_DEVICE = 0, 1, 2
 NULL_CT = 0xFFFFFFFF
 
 
@@ -98,6 +99,7 @@ _SIGS = {
     "fr_default_params": (C.c_int, [C.POINTER(Params)]),
     "fr_load_client_key": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "fr_gen_server_key": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "fr_set_keygen": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_export_server_key": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
     "fr_server_key_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
     "fr_encrypt_str": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint64, u64p]),
@@ -246,7 +248,13 @@ class Context:
         _check(lib().fr_load_client_key(self.h, blob, len(blob)))
 
     def gen_server_key(self, seed: int):
+        """ServerKey::new (engine.rs:252): on the GPU for the FFT ring (KEYGEN_AUTO),
+        else on the host; both give the same key bit for bit."""
         _check(lib().fr_gen_server_key(self.h, seed))
+
+    def set_keygen(self, where: int):
+        """KEYGEN_AUTO (device when present, FFT ring), KEYGEN_HOST or KEYGEN_DEVICE."""
+        _check(lib().fr_set_keygen(self.h, where))
 
     def export_server_key(self):
         a, b = C.c_size_t(), C.c_size_t()

@@ -106,12 +106,17 @@ int fr_default_params(fr_params* out); /* PARAM_MESSAGE_2_CARRY_2, k=1, N=2048 *
 /* ----- keys ----- */
 /* bincode RadixClientKey (tfhe-rs 0.2 layout, reference test_data/client_key). */
 int fr_load_client_key(fr_ctx* ctx, const uint8_t* bincode, size_t len);
-/* Deterministic server key (KSK mod 2^64, BSK mod Q) from the client key and a
- * seed (ServerKey::new, engine.rs:252); uploads it and converts the BSK to the
- * NTT domain on the device when the context has one. */
+/* Deterministic server key (KSK mod 2^64; BSK on the 2^64 torus for the FFT
+ * ring, mod Q for the RNS ring) from the client key and a seed
+ * (ServerKey::new, engine.rs:252; gen_keys_radix, ciphertext.rs:44).  With a
+ * device and the FFT ring it is generated on the GPU (FR_KEYGEN_AUTO); the
+ * host generator gives the same words bit for bit (fr_set_keygen). */
 int fr_gen_server_key(fr_ctx* ctx, uint64_t seed);
+enum { FR_KEYGEN_AUTO = 0, FR_KEYGEN_HOST = 1, FR_KEYGEN_DEVICE = 2 };
+int fr_set_keygen(fr_ctx* ctx, int32_t where);
 /* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = W*(k+1)^2*N u64
- * (coefficient domain mod Q = 998244353*1004535809, layout [w][row][component][coef]).
+ * (coefficient domain, torus 2^64 (FFT ring) or mod Q = 998244353*1004535809
+ * (RNS ring), layout [w][row][component][coef]).
  * k = 1: bootstrapping-key unrolling, W = 3*ceil(n/2) GGSWs, w = 3t+g encrypts
  * s_2t*s_2t+1, s_2t*(1-s_2t+1), (1-s_2t)*s_2t+1 for g = 0, 1, 2; k > 1: W = n,
  * GGSW w encrypts s_w.  Sizes from fr_server_key_sizes.  Either may be NULL. */
