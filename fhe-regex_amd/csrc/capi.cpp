@@ -514,17 +514,108 @@ int fr_encrypt_blocks(fr_ctx* ctx, const uint8_t* msgs, size_t count, uint64_t s
     })
 }
 
+// radix messages of a string (ciphertext.rs:18-29: 4 blocks of 2 bits, least significant first)
+// PARAM_MESSAGE_2_CARRY_2 (the only parameter family of the reference)
+constexpr uint64_t MESSAGE_MODULUS = 4, CARRY_MODULUS = 4;
+
+static std::vector<uint8_t> str_blocks(const char* s, size_t len) {
+    std::vector<uint8_t> msgs(4 * len);
+    for (size_t i = 0; i < len; ++i) {
+        const uint8_t c = (uint8_t)s[i];
+        if (c > 127) throw Error(FR_ERR_NON_ASCII, "content contains non-ascii characters");
+        for (int b = 0; b < 4; ++b) msgs[4 * i + b] = (c >> (2 * b)) & 3;
+    }
+    return msgs;
+}
+
 int fr_encrypt_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, uint64_t* out) {
     FR_TRY({
         NEED(ctx && (s || !len) && (out || !len));
         if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
-        std::vector<uint8_t> msgs(4 * len);
-        for (size_t i = 0; i < len; ++i) {
-            uint8_t c = (uint8_t)s[i];
-            if (c > 127) throw Error(FR_ERR_NON_ASCII, "content contains non-ascii characters");
-            for (int b = 0; b < 4; ++b) msgs[4 * i + b] = (c >> (2 * b)) & 3;  // ciphertext.rs:18-29
-        }
+        const std::vector<uint8_t> msgs = str_blocks(s, len);
         encrypt_blocks(ctx->p, ctx->ck, msgs.data(), msgs.size(), seed, 0, out);
+    })
+}
+
+int fr_encrypt_upload_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, fr_ct* out) {
+    FR_TRY({
+        NEED(ctx && (s || !len) && (out || !len));
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        Device& dev = ctx->device();
+        const std::vector<uint8_t> msgs = str_blocks(s, len);
+        std::vector<int> slots(msgs.size());
+        for (auto& x : slots) x = dev.alloc_slot();
+        try {
+            dev.encrypt_to_slots(ctx->ck, msgs.data(), msgs.size(), seed, 0, slots.data());
+        } catch (...) {
+            for (int x : slots) dev.free_slot(x);
+            throw;
+        }
+        for (size_t i = 0; i < len; ++i) {
+            HandleRec r;
+            for (int b = 0; b < 4; ++b) r.b[b].slot = slots[4 * i + b];
+            out[i] = ctx->new_handle(r);
+        }
+    })
+}
+
+// bincode (fixint, little endian) of tfhe-rs 0.2 RadixCiphertext:
+//   u64 n_blocks, then per block: u64 len, len x u64 LWE words, u64 degree,
+//   u64 message_modulus, u64 carry_modulus
+int fr_radix_serialize(fr_ctx* ctx, const uint64_t* blocks, size_t n_blocks, uint64_t degree, uint8_t* buf,
+                       size_t cap, size_t* written) {
+    FR_TRY({
+        NEED(ctx && (blocks || !n_blocks) && written);
+        const size_t L = (size_t)ctx->p.lwe_len();
+        const size_t need = 8 + n_blocks * (8 * (L + 4));
+        *written = need;
+        if (!buf) return FR_OK;  // size query
+        NEED(cap >= need);
+        uint8_t* o = buf;
+        auto put = [&](uint64_t v) {
+            std::memcpy(o, &v, 8);
+            o += 8;
+        };
+        put(n_blocks);
+        for (size_t b = 0; b < n_blocks; ++b) {
+            put(L);
+            std::memcpy(o, blocks + b * L, 8 * L);
+            o += 8 * L;
+            put(degree);
+            put(MESSAGE_MODULUS);
+            put(CARRY_MODULUS);
+        }
+    })
+}
+
+int fr_radix_deserialize(fr_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* blocks, size_t max_blocks,
+                         size_t* n_blocks) {
+    FR_TRY({
+        NEED(ctx && buf && n_blocks);
+        const size_t L = (size_t)ctx->p.lwe_len();
+        size_t off = 0;
+        auto get = [&]() -> uint64_t {
+            if (off + 8 > len) throw Error(FR_ERR_INVALID, "radix ciphertext: truncated");
+            uint64_t v;
+            std::memcpy(&v, buf + off, 8);
+            off += 8;
+            return v;
+        };
+        const uint64_t nb = get();
+        if (nb > (len - 8) / (8 * (L + 4))) throw Error(FR_ERR_INVALID, "radix ciphertext: bad block count");
+        *n_blocks = (size_t)nb;
+        if (!blocks) return FR_OK;  // size query
+        NEED(max_blocks >= nb);
+        for (uint64_t b = 0; b < nb; ++b) {
+            if (get() != L) throw Error(FR_ERR_INVALID, "radix ciphertext: LWE size does not match the parameters");
+            if (off + 8 * L > len) throw Error(FR_ERR_INVALID, "radix ciphertext: truncated");
+            std::memcpy(blocks + b * L, buf + off, 8 * L);
+            off += 8 * L;
+            (void)get();  // degree
+            if (get() != MESSAGE_MODULUS || get() != CARRY_MODULUS)
+                throw Error(FR_ERR_INVALID, "radix ciphertext: message/carry modulus does not match the parameters");
+        }
+        if (off != len) throw Error(FR_ERR_INVALID, "radix ciphertext: trailing bytes");
     })
 }
 

@@ -56,6 +56,10 @@ class Device {
     // device for download_server_key
     void gen_server_key(const ClientKey& ck, uint64_t seed);
     void download_server_key(uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
+    // fresh encryptions of block messages (encrypt_blocks, keys.h) written into
+    // allocated arena slots, bit-identical to the host encryption
+    void encrypt_to_slots(const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed, uint64_t first_block,
+                          const int* slots);
 
     // arena of big-LWE slots
     int alloc_slot();

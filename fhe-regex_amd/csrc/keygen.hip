@@ -179,6 +179,74 @@ __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict_
     }
 }
 
+// fresh LWE encryptions of block messages under the big key straight into
+// arena slots (encrypt_str, src/regex/ciphertext.rs:32-40):
+// one wave per block; masks are u64 numbers qb * kN + t of STREAM_ENC_MASK
+// (kN % 8 == 0: whole ChaCha blocks), body = <mask, s_big> + m 2^59 + noise
+__global__ void __launch_bounds__(64) k_encrypt_blocks(uint64_t seed, int big, const uint64_t* __restrict__ s_big,
+                                                       const uint8_t* __restrict__ msgs,
+                                                       const int64_t* __restrict__ noise, uint64_t first_block,
+                                                       const int* __restrict__ slots, int stride,
+                                                       uint64_t* __restrict__ arena) {
+    const int q = blockIdx.x, lane = threadIdx.x;
+    const uint64_t qb = first_block + q;
+    uint64_t* o = arena + (size_t)slots[q] * stride;
+    uint64_t acc = 0;
+    for (int b = lane; b < big / 8; b += 64) {
+        uint32_t w[16];
+        chacha_block(seed, STREAM_ENC_MASK, qb * (uint64_t)(big / 8) + b, w);
+#pragma unroll
+        for (int x = 0; x < 8; ++x) {
+            const uint64_t v = chacha_u64(w, x);
+            o[8 * b + x] = v;
+            acc += v * s_big[8 * b + x];
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) o[big] = acc + ((uint64_t)msgs[q] << DELTA_LOG) + (uint64_t)noise[q];
+}
+
+void Device::encrypt_to_slots(const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed,
+                              uint64_t first_block, const int* slots) {
+    if (!count) return;
+    const int big = p_.big();
+    if (big % 8) throw Error(FR_ERR_INVALID, "device encryption: kN must be a multiple of 8");
+    if (ck.s_big.size() != (size_t)big) throw Error(FR_ERR_INVALID, "device encryption: key size");
+    for (size_t i = 0; i < count; ++i)
+        if (slots[i] < 0 || (size_t)slots[i] >= next_slot_) throw Error(FR_ERR_INVALID, "device encryption: slot");
+    std::vector<int64_t> noise;
+    enc_noise(p_, seed, first_block, count, noise);
+    const hipStream_t s = (hipStream_t)stream_;
+    uint64_t* d_sb = nullptr;
+    uint8_t* d_m = nullptr;
+    int64_t* d_n = nullptr;
+    int* d_sl = nullptr;
+    auto cleanup = [&] {
+        (void)hipFree(d_sb);
+        (void)hipFree(d_m);
+        (void)hipFree(d_n);
+        (void)hipFree(d_sl);
+    };
+    try {
+        KG_CHECK(hipMalloc(&d_sb, 8 * (size_t)big));
+        KG_CHECK(hipMalloc(&d_m, count));
+        KG_CHECK(hipMalloc(&d_n, 8 * count));
+        KG_CHECK(hipMalloc(&d_sl, 4 * count));
+        KG_CHECK(hipMemcpyAsync(d_sb, ck.s_big.data(), 8 * (size_t)big, hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_m, msgs, count, hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_n, noise.data(), 8 * count, hipMemcpyHostToDevice, s));
+        KG_CHECK(hipMemcpyAsync(d_sl, slots, 4 * count, hipMemcpyHostToDevice, s));
+        k_encrypt_blocks<<<(unsigned)count, 64, 0, s>>>(seed, big, d_sb, d_m, d_n, first_block, d_sl, p_.slot_stride(),
+                                                       d_arena_);
+        KG_CHECK(hipGetLastError());
+        KG_CHECK(hipStreamSynchronize(s));
+    } catch (...) {
+        cleanup();
+        throw;
+    }
+    cleanup();
+}
+
 void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
     if (p_.ring != FR_RING_FFT || p_.N != 2048 || p_.k != 1)
         throw Error(FR_ERR_INVALID, "device keygen: FFT ring (k = 1, N = 2048) only");

@@ -281,6 +281,11 @@ void gen_bsk_noise_torus(const Params& p, uint64_t seed, std::vector<int32_t>& e
     });
     if (!ok) throw Error(FR_ERR_INVALID, "GLWE noise outside int32 (sigma too large for the device key generator)");
 }
+void enc_noise(const Params& p, uint64_t seed, uint64_t first_block, size_t count, std::vector<int64_t>& e) {
+    e.resize(count);
+    Rng rn(seed, STREAM_ENC_NOISE);
+    for (size_t q = 0; q < count; ++q) e[q] = rn.gaussian(first_block + q, p.glwe_sigma);
+}
 std::vector<uint8_t> ggsw_messages(const Params& p, const ClientKey& ck) {
     std::vector<uint8_t> m(p.bsk_ggsw());
     for (size_t w = 0; w < m.size(); ++w) m[w] = (uint8_t)ggsw_msg(p, ck, w);

@@ -59,6 +59,8 @@ void gen_bsk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<ui
 void gen_ksk_noise(const Params& p, uint64_t seed, std::vector<int64_t>& e);
 void gen_bsk_noise_torus(const Params& p, uint64_t seed, std::vector<int32_t>& e);
 std::vector<uint8_t> ggsw_messages(const Params& p, const ClientKey& ck);
+// noise of encrypt_blocks for blocks first_block .. first_block + count - 1
+void enc_noise(const Params& p, uint64_t seed, uint64_t first_block, size_t count, std::vector<int64_t>& e);
 
 // Fresh LWE encryptions of block messages (Delta = 2^59) under the big key.
 void encrypt_blocks(const Params& p, const ClientKey& ck, const uint8_t* msgs, size_t count, uint64_t seed,

@@ -108,6 +108,11 @@ _SIGS = {
     "fr_decode_block": (C.c_int, [C.c_void_p, u64p, C.POINTER(C.c_uint32)]),
     "fr_upload_radix": (C.c_int, [C.c_void_p, u64p, C.c_size_t, C.POINTER(C.c_uint32)]),
     "fr_upload_bool": (C.c_int, [C.c_void_p, u64p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "fr_encrypt_upload_str": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint64, C.POINTER(C.c_uint32)]),
+    "fr_radix_serialize": (C.c_int, [C.c_void_p, u64p, C.c_size_t, C.c_uint64, C.c_char_p, C.c_size_t,
+                                     C.POINTER(C.c_size_t)]),
+    "fr_radix_deserialize": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, u64p, C.c_size_t,
+                                       C.POINTER(C.c_size_t)]),
     "fr_download_radix": (C.c_int, [C.c_void_p, C.c_uint32, u64p]),
     "fr_release": (C.c_int, [C.c_void_p, C.c_uint32]),
     "fr_trivial": (C.c_int, [C.c_void_p, C.c_uint8, C.POINTER(C.c_uint32)]),
@@ -315,6 +320,30 @@ class Context:
         out = (C.c_uint32 * b.shape[0])()
         _check(lib().fr_upload_radix(self.h, _p(b), b.shape[0], out))
         return list(out)
+
+    def encrypt_upload_str(self, s: bytes | str, seed: int) -> List[int]:
+        """encrypt_str on the device into content handles (same words as encrypt_str)."""
+        if isinstance(s, str):
+            s = s.encode("latin-1")
+        out = (C.c_uint32 * len(s))()
+        _check(lib().fr_encrypt_upload_str(self.h, s, len(s), seed, out))
+        return list(out)
+
+    def serialize_radix(self, blocks: np.ndarray, degree: int = 3) -> bytes:
+        """bincode RadixCiphertext (tfhe-rs 0.2 layout, [ext] unverified) of one radix (4 blocks)."""
+        b = np.ascontiguousarray(blocks.reshape(-1, self.lwe_len), dtype=np.uint64)
+        n = C.c_size_t()
+        _check(lib().fr_radix_serialize(self.h, _p(b), b.shape[0], degree, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().fr_radix_serialize(self.h, _p(b), b.shape[0], degree, buf, n.value, C.byref(n)))
+        return buf.raw
+
+    def deserialize_radix(self, data: bytes) -> np.ndarray:
+        n = C.c_size_t()
+        _check(lib().fr_radix_deserialize(self.h, data, len(data), None, 0, C.byref(n)))
+        out = np.zeros((n.value, self.lwe_len), dtype=np.uint64)
+        _check(lib().fr_radix_deserialize(self.h, data, len(data), _p(out), n.value, C.byref(n)))
+        return out
 
     def upload_bool(self, lwes: np.ndarray) -> List[int]:
         b = np.ascontiguousarray(lwes.reshape(-1, self.lwe_len), dtype=np.uint64)

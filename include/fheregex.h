@@ -133,6 +133,20 @@ int fr_decode_block(fr_ctx* ctx, const uint64_t* lwe, uint32_t* msg_and_carry);
 /* ----- ciphertext arena ----- */
 int fr_upload_radix(fr_ctx* ctx, const uint64_t* blocks /* n*4*(kN+1) */, size_t n, fr_ct* out /* n */);
 int fr_upload_bool(fr_ctx* ctx, const uint64_t* lwe /* n*(kN+1) */, size_t n, fr_ct* out);
+/* encrypt_str (ciphertext.rs:32-40) on the device, straight into n_chars
+ * content handles: the same ciphertext words as fr_encrypt_str (same seed),
+ * without the host encryption and the 64 KB-per-char upload. */
+int fr_encrypt_upload_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, fr_ct* out /* len */);
+/* Wire format of a radix ciphertext: bincode (fixint, little endian) of tfhe-rs
+ * 0.2 RadixCiphertext — u64 n_blocks, then per block u64 len (= kN+1), the LWE
+ * words, u64 degree, u64 message_modulus (4), u64 carry_modulus (4).  [ext]
+ * unverified against tfhe-rs (absent here); follows the conventions of the
+ * verified client-key layout (Vec<u64> = u64 length + words, usize = u64).
+ * buf == NULL / blocks == NULL: size query only. */
+int fr_radix_serialize(fr_ctx* ctx, const uint64_t* blocks, size_t n_blocks, uint64_t degree, uint8_t* buf, size_t cap,
+                       size_t* written);
+int fr_radix_deserialize(fr_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* blocks, size_t max_blocks,
+                         size_t* n_blocks);
 int fr_download_radix(fr_ctx* ctx, fr_ct h, uint64_t* out /* 4*(kN+1) */);
 int fr_release(fr_ctx* ctx, fr_ct h);
 int fr_trivial(fr_ctx* ctx, uint8_t value, fr_ct* out);
