@@ -91,6 +91,13 @@ class Device {
   private:
     void ensure_arena(size_t slots);
     void ensure_batch(size_t n);
+    // pinned staging ring for gate descriptors: a buffer is rewritten only after
+    // its previous H2D copy completed (no stream-wide sync between levels)
+    DevGate* stage_acquire();
+    void stage_copy(size_t n);
+    // profiling: per-level event triples resolved at sync() (no sync per level)
+    void* take_event();
+    void resolve_timers();
     void ensure_digits(size_t rows);
     void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks);
     void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n);
@@ -130,7 +137,15 @@ class Device {
     std::vector<int> free_slots_;
     size_t next_slot_ = 0;
     DevGate* d_gates_ = nullptr;
-    DevGate* h_gates_ = nullptr;  // pinned staging
+    DevGate* h_stage_[2] = {nullptr, nullptr};  // pinned staging ring
+    void* stage_ev_[2] = {nullptr, nullptr};
+    int stage_ = 0;
+    struct PendingTimer {
+        void* ev[3];
+        size_t gates, outs;
+    };
+    std::vector<PendingTimer> pending_;
+    std::vector<void*> event_pool_;
     uint64_t* d_ks_ = nullptr;
     size_t batch_cap_ = 0;
     bool profiling_ = false;

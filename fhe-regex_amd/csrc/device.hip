@@ -946,6 +946,12 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         HIP_CHECK(hipEventCreate(&ev));
         e = ev;
     }
+    for (auto& e : stage_ev_) {
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        HIP_CHECK(hipEventRecord(ev, s));  // complete before first use
+        e = ev;
+    }
     // unrolled (k = 1) kernels keep three GGSW rows in registers: E = 8 only
     if (p.bsk_unroll() == 2) e_ = e_small_ = 8;
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
@@ -981,7 +987,13 @@ Device::~Device() {
     (void)hipFree(d_arena_);
     (void)hipFree(d_gates_);
     (void)hipFree(d_ks_);
-    if (h_gates_) (void)hipHostFree(h_gates_);
+    for (auto* h : h_stage_)
+        if (h) (void)hipHostFree(h);
+    for (auto* e : stage_ev_)
+        if (e) (void)hipEventDestroy((hipEvent_t)e);
+    for (auto& t : pending_)
+        for (auto* e : t.ev) (void)hipEventDestroy((hipEvent_t)e);
+    for (auto* e : event_pool_) (void)hipEventDestroy((hipEvent_t)e);
     for (auto e : ev_)
         if (e) (void)hipEventDestroy((hipEvent_t)e);
     if (stream_) (void)hipStreamDestroy(STREAM);
@@ -1029,9 +1041,12 @@ void Device::ensure_batch(size_t n) {
     HIP_CHECK(hipStreamSynchronize(STREAM));
     (void)hipFree(d_gates_);
     (void)hipFree(d_ks_);
-    if (h_gates_) (void)hipHostFree(h_gates_);
+    for (auto& h : h_stage_) {
+        if (h) (void)hipHostFree(h);
+        h = nullptr;
+    }
     HIP_CHECK(hipMalloc(&d_gates_, sizeof(DevGate) * cap));
-    HIP_CHECK(hipHostMalloc(&h_gates_, sizeof(DevGate) * cap));
+    for (auto& h : h_stage_) HIP_CHECK(hipHostMalloc(&h, sizeof(DevGate) * cap));
     HIP_CHECK(hipMalloc(&d_ks_, (size_t)8 * p_.ks_stride() * cap));
     batch_cap_ = cap;
 }
@@ -1191,40 +1206,75 @@ void Device::run_level(const DevGate* gates, size_t n) {
             if (g.in_slot[q] < 0 || (size_t)g.in_slot[q] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad input slot");
     }
     ensure_batch(n);
-    // the staging buffer may still be read by an in-flight copy
-    HIP_CHECK(hipStreamSynchronize(STREAM));
-    std::memcpy(h_gates_, gates, sizeof(DevGate) * n);
-    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof(DevGate) * n, hipMemcpyHostToDevice, STREAM));
-    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)ev_[0], STREAM));
+    // d_gates_ / d_ks_ are reused in stream order (this level's copy runs after
+    // the previous level's kernels); only the host staging buffer needs a wait
+    std::memcpy(stage_acquire(), gates, sizeof(DevGate) * n);
+    stage_copy(n);
+    PendingTimer t{};
+    if (profiling_) {
+        for (auto& e : t.ev) e = take_event();
+        HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[0], STREAM));
+    }
     launch_ks(d_gates_, n, d_ks_);
-    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)ev_[1], STREAM));
+    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[1], STREAM));
     launch_br(d_gates_, d_ks_, n);
     if (profiling_) {
-        HIP_CHECK(hipEventRecord((hipEvent_t)ev_[2], STREAM));
-        size_t outs = 0;
-        for (size_t i = 0; i < n; ++i) outs += gates[i].n_out;
-        timers_.lut_outputs += outs;
-        HIP_CHECK(hipEventSynchronize((hipEvent_t)ev_[2]));
+        HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[2], STREAM));
+        t.gates = n;
+        t.outs = 0;
+        for (size_t i = 0; i < n; ++i) t.outs += gates[i].n_out;
+        pending_.push_back(t);
+    }
+}
+
+DevGate* Device::stage_acquire() {
+    stage_ ^= 1;
+    HIP_CHECK(hipEventSynchronize((hipEvent_t)stage_ev_[stage_]));  // never-recorded events are complete
+    return h_stage_[stage_];
+}
+void Device::stage_copy(size_t n) {
+    HIP_CHECK(hipMemcpyAsync(d_gates_, h_stage_[stage_], sizeof(DevGate) * n, hipMemcpyHostToDevice, STREAM));
+    HIP_CHECK(hipEventRecord((hipEvent_t)stage_ev_[stage_], STREAM));
+}
+void* Device::take_event() {
+    if (!event_pool_.empty()) {
+        void* e = event_pool_.back();
+        event_pool_.pop_back();
+        return e;
+    }
+    hipEvent_t ev;
+    HIP_CHECK(hipEventCreate(&ev));
+    return ev;
+}
+// KS / BR kernel times of the levels issued since the last sync (HIP events
+// on the launch stream, read once the stream has drained)
+void Device::resolve_timers() {
+    for (auto& t : pending_) {
         float ks = 0, br = 0;
-        HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)ev_[0], (hipEvent_t)ev_[1]));
-        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)ev_[1], (hipEvent_t)ev_[2]));
+        HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)t.ev[0], (hipEvent_t)t.ev[1]));
+        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[1], (hipEvent_t)t.ev[2]));
         timers_.ks_ms += ks;
         timers_.br_ms += br;
         timers_.br_launches += 1;
-        timers_.br_gates += n;
+        timers_.br_gates += t.gates;
+        timers_.lut_outputs += t.outs;
+        for (auto* e : t.ev) event_pool_.push_back(e);
     }
+    pending_.clear();
 }
 
 void Device::run_linear(const DevGate& g) {
     ensure_batch(1);
-    HIP_CHECK(hipStreamSynchronize(STREAM));
-    std::memcpy(h_gates_, &g, sizeof g);
-    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof g, hipMemcpyHostToDevice, STREAM));
+    std::memcpy(stage_acquire(), &g, sizeof g);
+    stage_copy(1);
     k_linear<<<(p_.lwe_len() + 255) / 256, 256, 0, STREAM>>>(d_gates_, d_arena_, p_.slot_stride(), p_.lwe_len());
     HIP_CHECK(hipGetLastError());
 }
 
-void Device::sync() { HIP_CHECK(hipStreamSynchronize(STREAM)); }
+void Device::sync() {
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    resolve_timers();
+}
 
 // ---------------------------------------------------------------- tests
 void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
@@ -1346,9 +1396,9 @@ void Device::ring_mul_host(const uint64_t* a, const uint64_t* b, size_t count, u
 void Device::bench_pbs(const std::vector<DevGate>& gates, int iters, double* br_ms, double* total_ms) {
     const size_t n = gates.size();
     ensure_batch(n);
-    HIP_CHECK(hipStreamSynchronize(STREAM));
-    std::memcpy(h_gates_, gates.data(), sizeof(DevGate) * n);
-    HIP_CHECK(hipMemcpyAsync(d_gates_, h_gates_, sizeof(DevGate) * n, hipMemcpyHostToDevice, STREAM));
+    sync();
+    std::memcpy(stage_acquire(), gates.data(), sizeof(DevGate) * n);
+    stage_copy(n);
     float br_sum = 0;
     HIP_CHECK(hipEventRecord((hipEvent_t)ev_[3], STREAM));
     for (int it = 0; it < iters; ++it) {
