@@ -89,6 +89,62 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
     }
 }
 
+// Latency shape: a lane's twiddles are the same every step (they depend on the
+// lane, the stage and the element only), so they are read from LDS once and
+// kept in registers: LOG * E / 2 complex values, index (s, k-th butterfly of s).
+template <int M, int E>
+struct FTwr {
+    static constexpr int COUNT = FGeo<M, E>::LOG * (E / 2);
+    double2 v[COUNT];
+};
+template <int M, int E>
+constexpr int ftw_index(int s, int m) {
+    const int d = FGeo<M, E>::LOG - 1 - s - FGeo<M, E>::lo(s / FGeo<M, E>::e);
+    return s * (E / 2) + ((m >> (d + 1)) << d) + (m & ((1 << d) - 1));
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* tw, int tl) {
+    using G = FGeo<M, E>;
+    const int b = G::template base<p>(tl);
+#pragma unroll
+    for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+        const double2* zs = tw + (b >> (G::LOG - s));
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            twr.v[ftw_index<M, E>(s, m)] = zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))];
+        }
+    }
+    if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1>(twr, tw, tl);
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void ffwd_phase_r(double2 (&x)[E], const FTwr<M, E>& twr) {
+    using G = FGeo<M, E>;
+#pragma unroll
+    for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            cfwd(x[m], x[m + dm], twr.v[ftw_index<M, E>(s, m)]);
+        }
+    }
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void finv_phase_r(double2 (&x)[E], const FTwr<M, E>& twr) {
+    using G = FGeo<M, E>;
+#pragma unroll
+    for (int s = G::s_end(p) - 1; s >= G::s_begin(p); --s) {
+        const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            if (m & dm) continue;
+            cinv(x[m], x[m + dm], twr.v[ftw_index<M, E>(s, m)]);
+        }
+    }
+}
+
 // exchange between phase layouts stays inside each wave (see device.hip)
 template <int M, int E, int PF, int PT>
 constexpr bool fwave_local() {
@@ -155,6 +211,26 @@ __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, con
     if constexpr (p > 0) {
         fexchange<M, E, p, p - 1, !NOPRE && finv_pre<M, E, p>()>(x, row, tl);
         finverse_from<M, E, p - 1, NOPRE>(x, row, tw, tl);
+    }
+}
+
+// the same with register twiddles (latency shape)
+template <int M, int E, int p>
+__device__ __forceinline__ void fforward_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr,
+                                                int tl) {
+    ffwd_phase_r<M, E, p>(x, twr);
+    if constexpr (p + 1 < FGeo<M, E>::NPH) {
+        fexchange<M, E, p, p + 1, false>(x, row, tl);
+        fforward_from_r<M, E, p + 1>(x, row, twr, tl);
+    }
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void finverse_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr,
+                                                int tl) {
+    finv_phase_r<M, E, p>(x, twr);
+    if constexpr (p > 0) {
+        fexchange<M, E, p, p - 1, false>(x, row, tl);
+        finverse_from_r<M, E, p - 1>(x, row, twr, tl);
     }
 }
 
@@ -287,8 +363,11 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const double2* orow_bl = orow + G::template at<XL>(bl);
     constexpr size_t GG = 4 * (size_t)M;  // complex values per Fourier GGSW: [r][c][m][lane]
     const int steps = (n + 1) / 2;
-    // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other row][m]
+    // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other row][m],
+    // and the lane's twiddles
     double2 gv[3][2][LAT ? E : 1];
+    FTwr<M, LAT ? E : 2> twr;
+    if constexpr (LAT) ftw_load_phase<M, E, 0>(twr, tw, tl);
 #ifdef FR_BR_TIMING
     uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
@@ -321,7 +400,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
         FBR_STAMP(1);
         // 2. forward FFT
-        fforward_from<M, E, 0, LAT>(x, row, tw, tl);
+        if constexpr (LAT) fforward_from_r<M, E, 0>(x, row, twr, tl);
+        else fforward_from<M, E, 0, false>(x, row, tw, tl);
         FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #pragma unroll
@@ -402,7 +482,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
-        finverse_from<M, E, LAST, LAT>(x, irow, tw, tl);
+        if constexpr (LAT) finverse_from_r<M, E, LAST>(x, irow, twr, tl);
+        else finverse_from<M, E, LAST, false>(x, irow, tw, tl);
         FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
