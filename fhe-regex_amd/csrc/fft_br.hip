@@ -92,6 +92,14 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 // Latency shape: a lane's twiddles are the same every step (they depend on the
 // lane, the stage and the element only), so they are read from LDS once and
 // kept in registers: LOG * E / 2 complex values, index (s, k-th butterfly of s).
+// phases of the latency shape's forward FFT after which GGSW 1 and 2 are loaded
+#ifndef FR_LAT_LOAD1
+#define FR_LAT_LOAD1 2
+#endif
+#ifndef FR_LAT_LOAD2
+#define FR_LAT_LOAD2 3
+#endif
+
 template <int M, int E>
 struct FTwr {
     static constexpr int COUNT = FGeo<M, E>::LOG * (E / 2);
@@ -215,13 +223,15 @@ __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, con
 }
 
 // the same with register twiddles (latency shape)
-template <int M, int E, int p>
-__device__ __forceinline__ void fforward_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr,
-                                                int tl) {
+// hook(integral_constant<p>) runs after phase p's butterflies (before its exchange)
+template <int M, int E, int p, class Hook>
+__device__ __forceinline__ void fforward_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr, int tl,
+                                                Hook&& hook) {
     ffwd_phase_r<M, E, p>(x, twr);
+    hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
         fexchange<M, E, p, p + 1, false>(x, row, tl);
-        fforward_from_r<M, E, p + 1>(x, row, twr, tl);
+        fforward_from_r<M, E, p + 1>(x, row, twr, tl, hook);
     }
 }
 template <int M, int E, int p>
@@ -378,20 +388,22 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         FBR_STAMP(0);
         // (uniform base pointers in SGPRs + the lane offset: no per-load address VGPRs)
         const double2* bw = bsk + (size_t)(3 * __builtin_amdgcn_readfirstlane(t)) * GG;
-        if constexpr (LAT) {  // lands during the digits and the forward FFT
+        // latency shape: GGSW g's slots for this lane, issued in three groups spread
+        // over the forward FFT (one group per phase boundary) so that no wave stalls on
+        // a full load queue at the top of the step; they land before the MAC
+        auto load_ggsw = [&](int gg) {
 #pragma unroll
-            for (int gg = 0; gg < 3; ++gg)
-#pragma unroll
-                for (int m = 0; m < E; ++m) {
+            for (int m = 0; m < E; ++m) {
 #ifdef FR_FFT_NOBSK  // timing experiment only (wrong results): no GGSW traffic
-                    gv[gg][0][m] = make_double2(t + gg, m);
-                    gv[gg][1][m] = make_double2(m, t - gg);
+                gv[gg][0][m] = make_double2(t + gg, m);
+                gv[gg][1][m] = make_double2(m, t - gg);
 #else
-                    gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
-                    gv[gg][1][m] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+                gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
+                gv[gg][1][m] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
 #endif
-                }
-        }
+            }
+        };
+        if constexpr (LAT) load_ggsw(0);
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
         // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
         double2 x[E];
@@ -400,8 +412,23 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
         FBR_STAMP(1);
         // 2. forward FFT
-        if constexpr (LAT) fforward_from_r<M, E, 0>(x, row, twr, tl);
-        else fforward_from<M, E, 0, false>(x, row, tw, tl);
+        if constexpr (LAT) {
+            fforward_from_r<M, E, 0>(x, row, twr, tl, [&](auto ph) {
+                constexpr int p = decltype(ph)::value;
+                if constexpr (p == FR_LAT_LOAD1) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_ggsw(1);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if constexpr (p == FR_LAT_LOAD2) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    load_ggsw(2);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            });
+        } else {
+            fforward_from<M, E, 0, false>(x, row, tw, tl);
+        }
         FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #pragma unroll
