@@ -168,9 +168,109 @@ __device__ __forceinline__ void fwave_sync() {
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
+// Register exchanges.  An exchange between adjacent layouts transposes the lane's
+// element bits with the lane bits that carry the arriving index bits.  When element
+// bit j leaves through the same lane bit k that brings in the next layout's element
+// bit j, and k is 4 or 5 (row pairs / wave halves), the transpose of each pair
+// (A = x[m], B = x[m | 2^j]) is one v_permlane16/32_swap per dword: lanes with bit k
+// clear keep A and receive the partner's A as B; lanes with bit k set keep B and
+// receive the partner's B as A.  No LDS traffic and no barrier (E = 4: the exchange
+// between layouts 1 and 2 of both transforms).
+template <int M, int E, int PF, int PT>
+constexpr int fperm_lane_bit(int j) {
+    using G = FGeo<M, E>;
+    const int out = G::lo(PF) + j, in = G::lo(PT) + j;
+    int kb = -1, kc = -1;
+    for (int b = 0; b < 6; ++b) {
+        if (geo_lane_bit(G::LOG, G::e, PT, b) == out) kb = b;
+        if (geo_lane_bit(G::LOG, G::e, PF, b) == in) kc = b;
+    }
+    return kb == kc ? kb : -1;
+}
+#ifdef FR_FFT_DPP  // experiment: lane bits 0..3 by DPP moves + selects
+constexpr int FPERM_MIN_BIT = 0;
+#else
+constexpr int FPERM_MIN_BIT = 4;
+#endif
+template <int M, int E, int PF, int PT>
+constexpr bool fperm_ok() {
+#ifdef FR_FFT_NOPERM  // A/B switch: every exchange through LDS
+    return false;
+#else
+    using G = FGeo<M, E>;
+    if (PF == PT || (PF - PT != 1 && PT - PF != 1)) return false;
+    for (int j = 0; j < G::e; ++j) {
+        const int k = fperm_lane_bit<M, E, PF, PT>(j);
+        if (k < FPERM_MIN_BIT || k > 5) return false;
+    }
+    // every other lane bit carries the same index bit in both layouts
+    for (int b = 0; b < 8; ++b) {
+        bool swapped = false;
+        for (int j = 0; j < G::e; ++j) swapped |= fperm_lane_bit<M, E, PF, PT>(j) == b;
+        if (!swapped && geo_lane_bit(G::LOG, G::e, PF, b) != geo_lane_bit(G::LOG, G::e, PT, b)) return false;
+    }
+    return true;
+#endif
+}
+// lane bits 0..3: A' = bit ? (partner's B) : A, B' = bit ? B : (partner's A); the
+// partner is lane ^ 2^K: quad_perm for K = 0, 1, row_shr / row_shl by 2^K for K = 2, 3
+template <int K>
+__device__ __forceinline__ unsigned fdpp_down(unsigned v) {  // value of lane - 2^K (lanes with bit K set)
+    constexpr int ctrl = K == 0 ? 0xB1 : K == 1 ? 0x4E : 0x110 + (1 << K);
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ unsigned fdpp_up(unsigned v) {  // value of lane + 2^K (lanes with bit K clear)
+    constexpr int ctrl = K == 0 ? 0xB1 : K == 1 ? 0x4E : 0x100 + (1 << K);
+    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xF, 0xF, false);
+}
+template <int K>
+__device__ __forceinline__ void fperm_swap(double& a, double& b) {
+    if constexpr (K < 4) {
+        const bool hi = (__lane_id() >> K) & 1;
+        const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+        const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+        const unsigned a0 = (unsigned)ua, a1 = (unsigned)(ua >> 32), b0 = (unsigned)ub, b1 = (unsigned)(ub >> 32);
+        const unsigned na0 = hi ? fdpp_down<K>(b0) : a0, na1 = hi ? fdpp_down<K>(b1) : a1;
+        const unsigned nb0 = hi ? b0 : fdpp_up<K>(a0), nb1 = hi ? b1 : fdpp_up<K>(a1);
+        a = __longlong_as_double((long long)(((unsigned long long)na1 << 32) | na0));
+        b = __longlong_as_double((long long)(((unsigned long long)nb1 << 32) | nb0));
+        return;
+    }
+    const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
+    const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
+    unsigned lo0 = (unsigned)ua, hi0 = (unsigned)(ua >> 32), lo1 = (unsigned)ub, hi1 = (unsigned)(ub >> 32);
+    if constexpr (K == 4) {
+        const auto l = __builtin_amdgcn_permlane16_swap(lo0, lo1, false, false);
+        const auto h = __builtin_amdgcn_permlane16_swap(hi0, hi1, false, false);
+        lo0 = l[0], lo1 = l[1], hi0 = h[0], hi1 = h[1];
+    } else {
+        const auto l = __builtin_amdgcn_permlane32_swap(lo0, lo1, false, false);
+        const auto h = __builtin_amdgcn_permlane32_swap(hi0, hi1, false, false);
+        lo0 = l[0], lo1 = l[1], hi0 = h[0], hi1 = h[1];
+    }
+    a = __longlong_as_double((long long)(((unsigned long long)hi0 << 32) | lo0));
+    b = __longlong_as_double((long long)(((unsigned long long)hi1 << 32) | lo1));
+}
+template <int M, int E, int PF, int PT, int j = 0>
+__device__ __forceinline__ void fperm_exchange(double2 (&x)[E]) {
+    constexpr int K = fperm_lane_bit<M, E, PF, PT>(j);
+#pragma unroll
+    for (int m = 0; m < E; ++m) {
+        if (m & (1 << j)) continue;
+        fperm_swap<K>(x[m].x, x[m | (1 << j)].x);
+        fperm_swap<K>(x[m].y, x[m | (1 << j)].y);
+    }
+    if constexpr (j + 1 < FGeo<M, E>::e) fperm_exchange<M, E, PF, PT, j + 1>(x);
+}
+
 template <int M, int E, int PF, int PT, bool PRE>
 __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
     using G = FGeo<M, E>;
+    if constexpr (fperm_ok<M, E, PF, PT>()) {
+        fperm_exchange<M, E, PF, PT>(x);
+        return;
+    }
     constexpr int X = PF < PT ? PF : PT;
     double2* rf = row + G::template at<X>(G::template base<PF>(tl));
     double2* rt = row + G::template at<X>(G::template base<PT>(tl));
@@ -196,8 +296,7 @@ template <int M, int E, int X = 0>
 constexpr bool fexchanges_conflict_free() {
     using G = FGeo<M, E>;
     if constexpr (X + 1 >= G::NPH) return true;
-    else return G::template banks_distinct<X>(X) && G::template banks_distinct<X>(X + 1) &&
-                fexchanges_conflict_free<M, E, X + 1>();
+    else return G::template b128_exchange_ok<X>() && fexchanges_conflict_free<M, E, X + 1>();
 }
 // NOPRE: the rows of the forward transform + MAC and of the inverse transform
 // are separate buffers (latency shape).  Then no write needs a barrier before

@@ -359,15 +359,18 @@ static inline uint64_t mix(uint64_t h, uint64_t v) {
 }
 
 int ValueDag::add(const VNode& n) {
-    uint64_t h = mix(mix(mix(mix(mix(0, n.op), (uint64_t)(int64_t)n.a), (uint64_t)(int64_t)n.b), (uint64_t)n.pos), n.c);
-    auto& bucket = index_[h];
-    for (int id : bucket) {
-        const VNode& m = nodes[id];
-        if (m.op == n.op && m.a == n.a && m.b == n.b && m.pos == n.pos && m.c == n.c) return id;
-    }
-    nodes.push_back(n);
-    bucket.push_back((int)nodes.size() - 1);
-    return (int)nodes.size() - 1;
+    const uint64_t h =
+        mix(mix(mix(mix(mix(0, n.op), (uint64_t)(int64_t)n.a), (uint64_t)(int64_t)n.b), (uint64_t)n.pos), n.c);
+    return index_.find_or_add(
+        h,
+        [&](int id) {
+            const VNode& m = nodes[id];
+            return m.op == n.op && m.a == n.a && m.b == n.b && m.pos == n.pos && m.c == n.c;
+        },
+        [&] {
+            nodes.push_back(n);
+            return (int)nodes.size() - 1;
+        });
 }
 
 int ValueDag::eval(int id, const uint8_t* content, std::vector<int16_t>& memo) const {
@@ -401,27 +404,29 @@ int ValueDag::eval(int id, const uint8_t* content, std::vector<int16_t>& memo) c
 
 // ============================================================ Execution
 int Execution::key(Tag t, int64_t a, int64_t b) {
-    uint64_t h = mix(mix(mix(0, t), (uint64_t)a), (uint64_t)b);
-    auto& bucket = key_index_[h];
-    for (int id : bucket) {
-        const KeyRec& k = keys_[id];
-        if (k.t == t && k.a == a && k.b == b) return id;
-    }
-    keys_.push_back({t, a, b});
-    bucket.push_back((int)keys_.size() - 1);
-    return (int)keys_.size() - 1;
+    const uint64_t h = mix(mix(mix(0, t), (uint64_t)a), (uint64_t)b);
+    return key_index_.find_or_add(
+        h,
+        [&](int id) {
+            const KeyRec& k = keys_[id];
+            return k.t == t && k.a == a && k.b == b;
+        },
+        [&] {
+            keys_.push_back({t, a, b});
+            return (int)keys_.size() - 1;
+        });
 }
 int Execution::const_of(int k) const { return keys_[k].t == K_CONST ? (int)keys_[k].a : -1; }
 
 template <class F>
 Val Execution::with_cache(int k, F&& f) {  // execution.rs:212-222
-    auto it = cache_.find(k);
-    if (it != cache_.end()) {
+    if ((size_t)k < cache_.size() && cache_[k] >= 0) {
         ++cache_hits_;
-        return {it->second, k};
+        return {cache_[k], k};
     }
     ++ct_ops_;
     int v = f();
+    if ((size_t)k >= cache_.size()) cache_.resize(std::max<size_t>(2 * cache_.size(), (size_t)k + 1), -1);
     cache_[k] = v;
     return {v, k};
 }

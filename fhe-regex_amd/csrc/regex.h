@@ -48,6 +48,48 @@ struct GrammarScope {  // sets the thread's grammar for parse(pattern)
     int prev_;
 };
 
+// Open-addressing index of dense ids by a 64-bit hash (linear probing, load
+// <= 1/2): hash-consing of DAG nodes and Executed keys without per-bucket
+// allocations.  find_or_add(h, eq, add): eq(id) tests a candidate, add()
+// appends the new record and returns its id.
+class IdIndex {
+  public:
+    template <class Eq, class Add>
+    int find_or_add(uint64_t h, Eq&& eq, Add&& add) {
+        if (2 * (count_ + 1) > ids_.size()) grow();
+        const size_t mask = ids_.size() - 1;
+        for (size_t i = (size_t)h & mask;; i = (i + 1) & mask) {
+            if (ids_[i] < 0) {
+                const int id = add();
+                ids_[i] = id;
+                hs_[i] = h;
+                ++count_;
+                return id;
+            }
+            if (hs_[i] == h && eq(ids_[i])) return ids_[i];
+        }
+    }
+
+  private:
+    void grow() {
+        std::vector<int32_t> ids(ids_.empty() ? 1024 : 2 * ids_.size(), -1);
+        std::vector<uint64_t> hs(ids.size());
+        const size_t mask = ids.size() - 1;
+        for (size_t j = 0; j < ids_.size(); ++j)
+            if (ids_[j] >= 0) {
+                size_t i = (size_t)hs_[j] & mask;
+                while (ids[i] >= 0) i = (i + 1) & mask;
+                ids[i] = ids_[j];
+                hs[i] = hs_[j];
+            }
+        ids_.swap(ids);
+        hs_.swap(hs);
+    }
+    std::vector<int32_t> ids_;
+    std::vector<uint64_t> hs_;
+    size_t count_ = 0;
+};
+
 // ------------------------------------------------------------ value DAG
 // What the reference actually computes homomorphically: one node per distinct
 // computation (hash-consed); short-circuited ops return an operand's node.
@@ -63,7 +105,7 @@ struct ValueDag {
     int add(const VNode& n);
     int eval(int id, const uint8_t* content, std::vector<int16_t>& memo) const;
   private:
-    std::unordered_map<uint64_t, std::vector<int>> index_;
+    IdIndex index_;
 };
 
 // ------------------------------------------------------- Execution (symbolic)
@@ -97,10 +139,10 @@ class Execution {
     template <class F>
     Val with_cache(int key, F&& f);
     ValueDag& dag_;
-    std::unordered_map<uint64_t, std::vector<int>> key_index_;
+    IdIndex key_index_;
     struct KeyRec { Tag t; int64_t a, b; };
     std::vector<KeyRec> keys_;
-    std::unordered_map<int, int> cache_;  // key -> value
+    std::vector<int32_t> cache_;  // key id -> value id, -1 if not executed
     uint64_t ct_ops_ = 0, cache_hits_ = 0;
 };
 
