@@ -187,11 +187,6 @@ constexpr int fperm_lane_bit(int j) {
     }
     return kb == kc ? kb : -1;
 }
-#ifdef FR_FFT_DPP  // experiment: lane bits 0..3 by DPP moves + selects
-constexpr int FPERM_MIN_BIT = 0;
-#else
-constexpr int FPERM_MIN_BIT = 4;
-#endif
 template <int M, int E, int PF, int PT>
 constexpr bool fperm_ok() {
 #ifdef FR_FFT_NOPERM  // A/B switch: every exchange through LDS
@@ -201,7 +196,7 @@ constexpr bool fperm_ok() {
     if (PF == PT || (PF - PT != 1 && PT - PF != 1)) return false;
     for (int j = 0; j < G::e; ++j) {
         const int k = fperm_lane_bit<M, E, PF, PT>(j);
-        if (k < FPERM_MIN_BIT || k > 5) return false;
+        if (k != 4 && k != 5) return false;
     }
     // every other lane bit carries the same index bit in both layouts
     for (int b = 0; b < 8; ++b) {
@@ -212,31 +207,9 @@ constexpr bool fperm_ok() {
     return true;
 #endif
 }
-// lane bits 0..3: A' = bit ? (partner's B) : A, B' = bit ? B : (partner's A); the
-// partner is lane ^ 2^K: quad_perm for K = 0, 1, row_shr / row_shl by 2^K for K = 2, 3
-template <int K>
-__device__ __forceinline__ unsigned fdpp_down(unsigned v) {  // value of lane - 2^K (lanes with bit K set)
-    constexpr int ctrl = K == 0 ? 0xB1 : K == 1 ? 0x4E : 0x110 + (1 << K);
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xF, 0xF, false);
-}
-template <int K>
-__device__ __forceinline__ unsigned fdpp_up(unsigned v) {  // value of lane + 2^K (lanes with bit K clear)
-    constexpr int ctrl = K == 0 ? 0xB1 : K == 1 ? 0x4E : 0x100 + (1 << K);
-    return (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, ctrl, 0xF, 0xF, false);
-}
 template <int K>
 __device__ __forceinline__ void fperm_swap(double& a, double& b) {
-    if constexpr (K < 4) {
-        const bool hi = (__lane_id() >> K) & 1;
-        const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
-        const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
-        const unsigned a0 = (unsigned)ua, a1 = (unsigned)(ua >> 32), b0 = (unsigned)ub, b1 = (unsigned)(ub >> 32);
-        const unsigned na0 = hi ? fdpp_down<K>(b0) : a0, na1 = hi ? fdpp_down<K>(b1) : a1;
-        const unsigned nb0 = hi ? b0 : fdpp_up<K>(a0), nb1 = hi ? b1 : fdpp_up<K>(a1);
-        a = __longlong_as_double((long long)(((unsigned long long)na1 << 32) | na0));
-        b = __longlong_as_double((long long)(((unsigned long long)nb1 << 32) | nb0));
-        return;
-    }
+    static_assert(K == 4 || K == 5, "permlane swaps serve lane bits 4 and 5");
     const unsigned long long ua = (unsigned long long)__double_as_longlong(a);
     const unsigned long long ub = (unsigned long long)__double_as_longlong(b);
     unsigned lo0 = (unsigned)ua, hi0 = (unsigned)(ua >> 32), lo1 = (unsigned)ub, hi1 = (unsigned)(ub >> 32);
@@ -357,6 +330,13 @@ constexpr int fbr_threads() {
 //    CU (<= 80 KB of LDS each) hide each other's barriers and loads; a slot's
 //    GGSW values are loaded one slot ahead in the MAC; psi^k from the quadrant
 //    table (k < N/2) + quarter turns.
+// LDS slot of psi^k in the monomial table.  A lane's lookup index is k = e L mod 2N
+// with L = 1 + 4 brv(lane slot base), so the 16 lanes of a b128 read group share
+// k mod 32 (every lookup one bank quad: ~13-way conflicts).  Folding bits 5..9 into
+// the quad bits spreads them (1.8-way on average over e); a bijection on [0, 2^10)
+// blocks, so it serves the N-entry and the N/2-entry (quadrant) table alike.
+__device__ __forceinline__ int psi_slot(int k) { return k ^ ((k >> 6) & 15) ^ ((k >> 5) & 1); }
+
 template <int N, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
     return 16 * ((LAT ? 4 : 2) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (LAT ? (size_t)N : (size_t)N / 2)) +
@@ -431,7 +411,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const int n_out = gates[g].n_out;
     const int kind = gates[g].direct;
     for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
-    for (int i = tid; i < NPSI; i += NT) psi[i] = psi_g[i];
+    for (int i = tid; i < NPSI; i += NT) psi[psi_slot(i)] = psi_g[i];
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
@@ -555,13 +535,13 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
                     const double2 c = make_double2((double)k, 0.5);
 #else
-                    const double2 c = psi[k & (N - 1)];
+                    const double2 c = psi[psi_slot((int)(k & (N - 1)))];
 #endif
                     const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
                     bre[h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
                     bim[h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
                 } else {
-                    const double2 q = psi[k & (N / 2 - 1)];
+                    const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
                     fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h][bb], bim[h][bb]);
                 }
             }

@@ -267,30 +267,32 @@ struct Lowerer {
         return f;
     }
     // literals of f as members of an AND (is_and) or OR list
-    std::vector<Lit> members(const Form& f0, bool is_and) {
-        if (f0.k == Form::SET) return members(expand_set(f0), is_and);
-        const Form& f = f0;
+    // (f is consumed: a same-kind form hands over its literal list)
+    std::vector<Lit> members(Form&& f, bool is_and) {
+        if (f.k == Form::SET) return members(expand_set(f), is_and);
         if (f.k == Form::CONST) throw Error(FR_ERR_INVALID, "lowering: constant member");
         if (f.k == Form::LIT) return {f.lit};
-        if ((f.k == Form::AND) == is_and) return f.lits;
+        if ((f.k == Form::AND) == is_and) return std::move(f.lits);
         return {materialize(f)};
     }
-    Form combine(bool is_and, const Form& a0, const Form& b0) {
+    // operands by value: lower_t moves a node's form in at its last use, so the long
+    // AND/OR chains of has_match grow their literal lists without copies
+    Form combine(bool is_and, Form a0, Form b0) {
         // same-position character sets combine exactly
         if (a0.k == Form::SET && b0.k == Form::SET && a0.pos == b0.pos) {
-            Form f = a0;
-            f.set = is_and ? (a0.set & b0.set) : (a0.set | b0.set);
+            Form f = std::move(a0);
+            f.set = is_and ? (f.set & b0.set) : (f.set | b0.set);
             if (f.set.none()) return const_form(0);
             if (f.set.all()) return const_form(1);
             return f;
         }
-        const Form a = a0.k == Form::SET ? expand_set(a0) : a0;
-        const Form b = b0.k == Form::SET ? expand_set(b0) : b0;
+        Form a = a0.k == Form::SET ? expand_set(a0) : std::move(a0);
+        Form b = b0.k == Form::SET ? expand_set(b0) : std::move(b0);
         // constant folding (booleans)
-        if (a.k == Form::CONST) return is_and ? (a.c ? b : const_form(0)) : (a.c ? const_form(1) : b);
-        if (b.k == Form::CONST) return is_and ? (b.c ? a : const_form(0)) : (b.c ? const_form(1) : a);
+        if (a.k == Form::CONST) return is_and ? (a.c ? std::move(b) : const_form(0)) : (a.c ? const_form(1) : std::move(b));
+        if (b.k == Form::CONST) return is_and ? (b.c ? std::move(a) : const_form(0)) : (b.c ? const_form(1) : std::move(a));
         // member lists are sorted (forms keep their literals sorted): merge, O(|a|+|b|)
-        const std::vector<Lit> l0 = members(a, is_and), r = members(b, is_and);
+        const std::vector<Lit> l0 = members(std::move(a), is_and), r = members(std::move(b), is_and);
         std::vector<Lit> l;
         l.reserve(l0.size() + r.size());
         std::merge(l0.begin(), l0.end(), r.begin(), r.end(), std::back_inserter(l));
@@ -319,8 +321,22 @@ struct Lowerer {
     }
 
     // ---------------------------------------------------------- threshold
+    std::vector<int32_t> uses;  // remaining AND/OR/NOT operand uses of each node (lower_t)
+    Form take(int id) {
+        if (--uses[id] <= 0) return std::move(memo[id]);
+        return memo[id];
+    }
     Form lower_t(int id) {
         if (done[id]) return memo[id];
+        uses.assign(dag.nodes.size(), 0);
+        for (const VNode& n : dag.nodes)
+            if (n.op == VNode::AND || n.op == VNode::OR) {
+                ++uses[n.a];
+                ++uses[n.b];
+            } else if (n.op == VNode::NOT) {
+                ++uses[n.a];
+            }
+        ++uses[id];  // the root's form is returned
         // iterative post-order over AND/OR/NOT chains to avoid deep recursion
         std::vector<int> st{id};
         while (!st.empty()) {
@@ -350,9 +366,17 @@ struct Lowerer {
                     else f.set = all >> (255 - n.c);
                     break;
                 }
-                case VNode::AND: f = combine(true, memo[n.a], memo[n.b]); break;
-                case VNode::OR: f = combine(false, memo[n.a], memo[n.b]); break;
-                case VNode::NOT: f = negate(memo[n.a]); break;
+                case VNode::AND: {
+                    Form fa = take(n.a);
+                    f = combine(true, std::move(fa), take(n.b));
+                    break;
+                }
+                case VNode::OR: {
+                    Form fa = take(n.a);
+                    f = combine(false, std::move(fa), take(n.b));
+                    break;
+                }
+                case VNode::NOT: f = negate(take(n.a)); break;
             }
             memo[x] = std::move(f);
             done[x] = 1;
@@ -481,7 +505,7 @@ Program lower(const ValueDag& dag, int root, int mode) {
     Program out;
     for (size_t g = 0; g < p.gates.size(); ++g) {
         if (!live[g]) continue;
-        PGate ng = p.gates[g];
+        PGate ng = std::move(p.gates[g]);
         for (auto& in : ng.ins)
             if (in.src >= 0) in.src = remap[in.src];
         remap[g] = (int)out.gates.size();
