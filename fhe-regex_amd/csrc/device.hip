@@ -958,6 +958,8 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_KS_MFMA")) ks_mfma_ = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("FR_KS_TILES")) ks_tiles_ = std::max(1, std::atoi(ev));
+    if (const char* ev = std::getenv("FR_KS_MR4_MIN")) ks_mr4_min_ = (size_t)std::atol(ev);
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -1140,7 +1142,7 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
     if (ks_mfma_) {
         const int KD = p_.big() * p_.ks_level;
         if (KD % 256) throw Error(FR_ERR_INVALID, "MFMA keyswitch needs kN*ks_level % 256 == 0");
-        const int MR = n >= 128 ? 4 : 1;  // row tiles per wave
+        const int MR = n >= ks_mr4_min_ ? 4 : 1;  // row tiles per wave
         const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
         if (bp > n) HIP_CHECK(hipMemsetAsync(d_dig_ + n * KD, 0, (bp - n) * KD, STREAM));
@@ -1151,7 +1153,7 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         // split K so that small batches still put ~2 waves on every SIMD
         const int tiles = (int)(bp / (32 * MR)) * (kl_cols_ / 32);
         int split = 1;
-        while (split < 16 && tiles * split < 2048 && (KD / 256) % (split * 2) == 0) split *= 2;
+        while (split < 16 && tiles * split < ks_tiles_ && (KD / 256) % (split * 2) == 0) split *= 2;
         const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)(kl_cols_ / 128), (unsigned)split);
         if (MR == 4)
             k_ks_mfma<4><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
