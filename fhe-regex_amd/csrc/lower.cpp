@@ -74,14 +74,19 @@ struct Lowerer {
     std::vector<Form> memo;
     std::vector<char> done;
 
-    Lowerer(const ValueDag& d, int m) : dag(d), mode(m), memo(d.nodes.size()), done(d.nodes.size(), 0) {}
+    Lowerer(const ValueDag& d, int m) : dag(d), mode(m), memo(d.nodes.size()), done(d.nodes.size(), 0) {
+        const size_t hint = std::min<size_t>(2 * d.nodes.size(), (size_t)1 << 18);  // bounded for huge DAGs
+        gate_index.reserve(hint);
+        set_memo.reserve(hint / 2);
+        prog.gates.reserve(hint);
+    }
 
-    int add_gate(const std::vector<int64_t>& key, PGate g) {
+    int add_gate(std::vector<int64_t>&& key, PGate&& g) {
         auto it = gate_index.find(key);
         if (it != gate_index.end()) return it->second;
         prog.gates.push_back(std::move(g));
         int id = (int)prog.gates.size() - 1;
-        gate_index[key] = id;
+        gate_index.emplace(std::move(key), id);
         return id;
     }
     // [x_{2h} + 4 x_{2h+1} ? v] over the packed nibble of char `pos`
@@ -90,16 +95,19 @@ struct Lowerer {
         g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
         if (kind == 0) lut_eq(g.lut, v);
         else lut_sign(g.lut, v);
-        return add_gate({1, kind, pos, half, v, tag}, g);
+        return add_gate({1, kind, pos, half, v, tag}, std::move(g));
     }
     // arbitrary 16-entry LUT over the packed nibble (x_{2h} + 4 x_{2h+1}) of char `pos`
     int nibble_lut_gate(int pos, int half, const uint8_t* lut) {
+        std::vector<int64_t> key(19);  // (offset 0, LUT kind)
+        key[0] = 6, key[1] = pos, key[2] = half;
+        for (int v = 0; v < 16; ++v) key[3 + v] = lut[v];
+        auto it = gate_index.find(key);
+        if (it != gate_index.end()) return it->second;
         PGate g;
         g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
         std::memcpy(g.lut, lut, 16);
-        std::vector<int64_t> key{6, pos, half};  // (offset 0, LUT kind)
-        for (int v = 0; v < 16; ++v) key.push_back(lut[v]);
-        return add_gate(key, g);
+        return add_gate(std::move(key), std::move(g));
     }
     // Lower "char at pos is in S" (S != {} and S != all).  Characters split into
     // nibbles (hi, lo); rows = hi values grouped by their lo-set, columns = lo
@@ -180,7 +188,7 @@ struct Lowerer {
             }
             std::vector<int64_t> key{7, gh, gl, Cn};
             for (int v = 0; v < 16; ++v) key.push_back(g.lut[v]);
-            return lit_form(Lit{add_gate(key, g), false});
+            return lit_form(Lit{add_gate(std::move(key), std::move(g)), false});
         }
         Form f;
         f.k = Form::OR;
@@ -229,7 +237,7 @@ struct Lowerer {
         }
         const int m = (int)lits.size();
         g.offset = 2 * negs + (is_and ? 1 - 2 * m : -1);
-        return add_gate(key, g);
+        return add_gate(std::move(key), std::move(g));
     }
     Lit materialize(const Form& f0) {
         if (f0.k == Form::SET) return materialize(expand_set(f0));
@@ -389,7 +397,7 @@ struct Lowerer {
         PGate g;
         g.ins = {{hi, 3}, {lo, 1}};
         lut_gt3(g.lut, n.op == VNode::LE);
-        return add_gate({3, n.op, n.pos, n.c, tag}, g);
+        return add_gate({3, n.op, n.pos, n.c, tag}, std::move(g));
     }
 
     // ---------------------------------------------------------- faithful
@@ -418,7 +426,7 @@ struct Lowerer {
                     PGate g;
                     g.ins = {{lo, 1}, {hi, 1}};
                     lut_eq(g.lut, 2);
-                    f = lit_form(Lit{add_gate({4, n.pos, n.c}, g), false});
+                    f = lit_form(Lit{add_gate({4, n.pos, n.c}, std::move(g)), false});
                     break;
                 }
                 case VNode::GT:
@@ -443,7 +451,7 @@ struct Lowerer {
                     g.offset = 2 * offset;
                     if (is_and) lut_eq(g.lut, 2);
                     else lut_at_least(g.lut, 1);
-                    f = lit_form(Lit{add_gate(key, g), false});
+                    f = lit_form(Lit{add_gate(std::move(key), std::move(g)), false});
                     break;
                 }
                 case VNode::NOT: f = negate(memo[n.a]); break;  // smart_bitxor(a, 1) on a boolean: linear
