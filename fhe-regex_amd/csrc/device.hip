@@ -812,52 +812,66 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
 // share the gate rows through L1, and the MR row tiles of a wave share each KSK
 // fragment (MR-fold less KSK traffic).  Partial results are subtracted from out
 // (pre-set to [t == n] * body) with 64-bit atomics: exact mod 2^64 in any order.
-template <int MR>
+template <int MR, int MC>
 __global__ void __launch_bounds__(256)
 k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, int KD, int ncols /* n + 1 */,
           int nlc /* limb-columns, multiple of 32 */, unsigned long long* __restrict__ out, int out_stride) {
-    constexpr int UN = MR == 1 ? 8 : 2;  // k-steps in flight per wave
+    constexpr int UN = MR * MC == 1 ? 8 : 2;  // k-steps in flight per wave
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
     const int g0 = blockIdx.x * 32 * MR;
-    const int lc0 = (blockIdx.y * 4 + w) * 32;
-    if (lc0 >= nlc) return;  // whole wave
+    const int lcw = (blockIdx.y * 4 + w) * 32 * MC;  // first limb-column of this wave's MC column tiles
+    if (lcw >= nlc) return;  // whole wave
     const int kspan = KD / gridDim.z, kb = blockIdx.z * kspan;
     const int8_t* ap = dig + (size_t)(g0 + r) * KD + 16 * h + kb;
-    const int8_t* bp = kl + (size_t)(lc0 + r) * KD + 16 * h + kb;
-    v16i_t acc[MR];
+    const int8_t* bp[MC];
 #pragma unroll
-    for (int t = 0; t < MR; ++t) acc[t] = v16i_t{0};
+    for (int c = 0; c < MC; ++c)  // a tile past the padded columns re-reads the last one (its result is dropped)
+        bp[c] = kl + (size_t)(min(lcw + 32 * c, nlc - 32) + r) * KD + 16 * h + kb;
+    v16i_t acc[MR][MC];
+#pragma unroll
+    for (int t = 0; t < MR; ++t)
+#pragma unroll
+        for (int c = 0; c < MC; ++c) acc[t][c] = v16i_t{0};
     for (int k0 = 0; k0 < kspan; k0 += 32 * UN) {  // kspan is a multiple of 256 (host)
-        v4i_t a[UN][MR], b[UN];
+        v4i_t a[UN][MR], b[UN][MC];
 #pragma unroll
         for (int u = 0; u < UN; ++u) {
-            b[u] = *(const v4i_t*)(bp + k0 + 32 * u);
+#pragma unroll
+            for (int c = 0; c < MC; ++c) b[u][c] = *(const v4i_t*)(bp[c] + k0 + 32 * u);
 #pragma unroll
             for (int t = 0; t < MR; ++t) a[u][t] = *(const v4i_t*)(ap + (size_t)t * 32 * KD + k0 + 32 * u);
         }
 #pragma unroll
         for (int u = 0; u < UN; ++u)
 #pragma unroll
-            for (int t = 0; t < MR; ++t) acc[t] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u][t], b[u], acc[t], 0, 0, 0);
+            for (int t = 0; t < MR; ++t)
+#pragma unroll
+                for (int c = 0; c < MC; ++c)
+                    acc[t][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u][t], b[u][c], acc[t][c], 0, 0, 0);
     }
-    // lane holds D[row][lc0 + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
-    // column (lc0 + r) / 8; sum the 8 limbs of a column across lanes r^1, r^2, r^4
-    const int limb = r & 7, col = (lc0 + r) >> 3;
+    // lane holds D[row][lc + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
+    // column (lc + r) / 8; sum the 8 limbs of a column across lanes r^1, r^2, r^4
+    const int limb = r & 7;
 #pragma unroll
-    for (int t = 0; t < MR; ++t)
+    for (int c = 0; c < MC; ++c) {
+        const int lc = lcw + 32 * c, col = (lc + r) >> 3;
+        if (lc >= nlc) continue;  // uniform
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            uint64_t v = (uint64_t)(int64_t)acc[t][i] << (8 * limb);
+        for (int t = 0; t < MR; ++t)
 #pragma unroll
-            for (int s = 1; s < 8; s <<= 1) {
-                const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
-                v += ((uint64_t)hi << 32) | lo;
+            for (int i = 0; i < 16; ++i) {
+                uint64_t v = (uint64_t)(int64_t)acc[t][c][i] << (8 * limb);
+#pragma unroll
+                for (int s = 1; s < 8; s <<= 1) {
+                    const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
+                    v += ((uint64_t)hi << 32) | lo;
+                }
+                const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (limb == 0 && g < B && col < ncols && v != 0)
+                    atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
             }
-            const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (limb == 0 && g < B && col < ncols && v != 0)
-                atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
-        }
+    }
 }
 
 // KSK (u64 [k][t], t <= n) -> balanced byte limbs [t*8 + l][k]
@@ -960,6 +974,7 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_KS_MFMA")) ks_mfma_ = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("FR_KS_TILES")) ks_tiles_ = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("FR_KS_MR4_MIN")) ks_mr4_min_ = (size_t)std::atol(ev);
+    if (const char* ev = std::getenv("FR_KS_MC")) ks_mc_ = std::atoi(ev);
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -1150,17 +1165,24 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         k_ks_digits<3, 5><<<dim3(8, (unsigned)n), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
                                                                      p_.big(), d_dig_, d_ks + p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
+        // column tiles per wave (A-fragment reuse; auto: two from 512 gates, where the
+        // traffic of re-read digit rows dominates: 178 -> 157 us at 512, 609 -> 472 us at 2048)
+        const int MC = MR != 4 ? 1 : ks_mc_ == 1 || ks_mc_ == 2 ? ks_mc_ : n >= 512 ? 2 : 1;
         // split K so that small batches still put ~2 waves on every SIMD
         const int tiles = (int)(bp / (32 * MR)) * (kl_cols_ / 32);
+        const int target = MC == 2 && ks_tiles_ == 2048 ? 8192 : ks_tiles_;
         int split = 1;
-        while (split < 16 && tiles * split < ks_tiles_ && (KD / 256) % (split * 2) == 0) split *= 2;
-        const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)(kl_cols_ / 128), (unsigned)split);
-        if (MR == 4)
-            k_ks_mfma<4><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
-                                                   (unsigned long long*)d_ks, p_.ks_stride());
+        while (split < 16 && tiles * split < target && (KD / 256) % (split * 2) == 0) split *= 2;
+        const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)((kl_cols_ + 128 * MC - 1) / (128 * MC)), (unsigned)split);
+        if (MR == 4 && MC == 2)
+            k_ks_mfma<4, 2><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                                      (unsigned long long*)d_ks, p_.ks_stride());
+        else if (MR == 4)
+            k_ks_mfma<4, 1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                                      (unsigned long long*)d_ks, p_.ks_stride());
         else
-            k_ks_mfma<1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
-                                                   (unsigned long long*)d_ks, p_.ks_stride());
+            k_ks_mfma<1, 1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                                      (unsigned long long*)d_ks, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         return;
     }

@@ -68,10 +68,11 @@ def test_keyswitch_bit_exact(gctx, oracle_k1):
     assert (got == exp).all()
 
 
-@pytest.mark.parametrize("count", [1, 130, 300])
+@pytest.mark.parametrize("count", [1, 130, 300, 600])
 def test_keyswitch_batch_sizes_bit_exact(gctx, oracle_k1, count):
     """MFMA keyswitch paths: split-K single rows (1), 4-row-tile blocking with
-    padding (130 -> 256 rows), and larger batches; random (non-message) masks."""
+    padding (130 -> 256 rows), larger batches, and two column tiles per wave
+    (600 >= 512, 640 padded rows); random (non-message) masks."""
     rng = np.random.default_rng(count)
     blocks = rng.integers(0, 2**64 - 1, (count, gctx.lwe_len), dtype=np.uint64, endpoint=True)
     got = gctx.dev_keyswitch(blocks)

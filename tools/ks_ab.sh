@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-for v in "FR_KS_TILES=2048" "FR_KS_TILES=8192" "FR_KS_TILES=32768" "FR_KS_TILES=8192 FR_KS_MR4_MIN=100000" "FR_KS_TILES=32768 FR_KS_MR4_MIN=100000"; do
+for v in "FR_KS_MC=1" "FR_KS_MC=2" "FR_KS_MC=2 FR_KS_TILES=8192" "FR_KS_MR4_MIN=100000"; do
   d=gpurun_out/ks_ab/$(echo $v | tr ' =' '__')
   mkdir -p $d
   env $v timeout -k 10 120 rocprofv3 --kernel-trace --stats -d $d -o run --output-format csv -- python3 bench.py --steps 3 --warmup 1 --cpu-sample 0 > $d/log 2>&1 || { echo "fail $v"; exit 1; }
