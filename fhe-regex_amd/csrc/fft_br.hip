@@ -241,19 +241,21 @@ template <int M, int E, int PF, int PT, bool PRE>
 __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
     using G = FGeo<M, E>;
     if constexpr (fperm_ok<M, E, PF, PT>()) {
+        // a pre-barrier would also order the next exchange's writes: keep the plan's barriers
+        static_assert(!PRE, "register exchanges replace only exchanges without a pre-barrier");
         fperm_exchange<M, E, PF, PT>(x);
-        return;
+    } else {
+        constexpr int X = PF < PT ? PF : PT;
+        double2* rf = row + G::template at<X>(G::template base<PF>(tl));
+        double2* rt = row + G::template at<X>(G::template base<PT>(tl));
+        if constexpr (PRE) __syncthreads();
+#pragma unroll
+        for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+        if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
+        else __syncthreads();
+#pragma unroll
+        for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
     }
-    constexpr int X = PF < PT ? PF : PT;
-    double2* rf = row + G::template at<X>(G::template base<PF>(tl));
-    double2* rt = row + G::template at<X>(G::template base<PT>(tl));
-    if constexpr (PRE) __syncthreads();
-#pragma unroll
-    for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
-    if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
-    else __syncthreads();
-#pragma unroll
-    for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
 }
 // barrier plan as in device.hip: only the first exchange of a transform and
 // exchanges writing a non-wave-top layout wait before writing
