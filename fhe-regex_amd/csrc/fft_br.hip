@@ -522,11 +522,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #else
         constexpr bool PRE0 = !LAT;  // slot 0 lands during the MAC barrier and row exchange
 #endif
-#ifdef FR_TP_ROLL  // experiment: each consumed GGSW's registers reload slot m + 1 (needs PRE0)
-        constexpr bool ROLL = PRE0 && !AHEAD;
-#else
-        constexpr bool ROLL = false;
-#endif
         double2 Bc[3][2];
         if constexpr (PRE0) load_slot<M, T>(Bc, bw, P, 0, tl);
         __syncthreads();
@@ -563,7 +558,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             if constexpr (AHEAD) {
                 if (m + 1 < E) load_slot<M, T>(Bn, bw, P, m + 1, tl);
                 __builtin_amdgcn_sched_barrier(0);
-            } else if constexpr (!LAT && !ROLL) {
+            } else if constexpr (!LAT) {
                 if (!PRE0 || m > 0) load_slot<M, T>(Bc, bw, P, m, tl);
             }
             const double2 own = x[m], oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
@@ -584,15 +579,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 fft::cmac(oth.x, oth.y, Bx.x, Bx.y, yr, yi);
                 if (gg == 0) fft::cmul(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
                 else fft::cmac(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
-                if constexpr (ROLL) {
-                    // GGSW gg of slot m is consumed: its registers take slot m + 1's values
-                    if (m + 1 < E) {
-                        __builtin_amdgcn_sched_barrier(0);
-                        constexpr size_t GGr = 4 * (size_t)M;
-                        Bc[gg][0] = (bw + (size_t)gg * GGr + (size_t)(3 * P) * M + (size_t)(m + 1) * T)[tl];
-                        Bc[gg][1] = (bw + (size_t)gg * GGr + (size_t)(2 - P) * M + (size_t)(m + 1) * T)[tl];
-                    }
-                }
             }
             x[m] = make_double2(zr, zi);
             if constexpr (!LAT) {
