@@ -275,10 +275,21 @@ struct NttGeo {
         }
         return true;
     }
+    // map X sends the N indices of a row to distinct addresses inside the row (NP slots)
+    template <int X>
+    static constexpr bool map_injective() {
+        bool seen[NP] = {};
+        for (int i = 0; i < N; ++i) {
+            const int a = at<X>(i);
+            if (a < 0 || a >= NP || seen[a]) return false;
+            seen[a] = true;
+        }
+        return true;
+    }
     template <int X>
     static constexpr bool b128_exchange_ok() {
         const int xt = X + 1 < NPH ? X + 1 : X;
-        return MAPS.m[X].span > 0 && b128_layout_ok<X>(X, true) && b128_layout_ok<X>(xt, false) &&
+        return MAPS.m[X].span > 0 && map_injective<X>() && b128_layout_ok<X>(X, true) && b128_layout_ok<X>(xt, false) &&
                b128_layout_ok<X>(xt, true) && b128_layout_ok<X>(X, false);
     }
     // element m of lane tl in phase p: idx = base(tl) | moff(m), disjoint bits,
