@@ -486,6 +486,31 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         };
         if constexpr (LAT) load_ggsw(0);
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
+        const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
+        constexpr int NB = E / 4;
+        double bre[2][NB], bim[2][NB];
+        auto psi_factors = [&]() {
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+#pragma unroll
+                for (int bb = 0; bb < NB; ++bb) {
+                    const uint32_t k = __umul24(h == 0 ? ei : ej, Lb[bb]) & (2 * N - 1);
+                    if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
+#ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
+                        const double2 c = make_double2((double)k, 0.5);
+#else
+                        const double2 c = psi[psi_slot((int)(k & (N - 1)))];
+#endif
+                        const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
+                        bre[h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
+                        bim[h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
+                    } else {
+                        const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
+                        fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h][bb], bim[h][bb]);
+                    }
+                }
+        };
+        if constexpr (LAT) psi_factors();
         // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
         double2 x[E];
 #pragma unroll
@@ -530,28 +555,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // slots of equal m >> 2 (E/4 bases per lane) and s_m = brv2(m & 3) (fft.h: L(j) =
         // 1 + 4 brv(j)).  psi^(1024 s e) = i^(s e) is an exact quarter turn (the table
         // itself is quadrant-reduced), so one lookup per (e, base) serves every slot.
-        const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
-        constexpr int NB = E / 4;
-        double bre[2][NB], bim[2][NB];
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int bb = 0; bb < NB; ++bb) {
-                const uint32_t k = __umul24(h == 0 ? ei : ej, Lb[bb]) & (2 * N - 1);
-                if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
-#ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
-                    const double2 c = make_double2((double)k, 0.5);
-#else
-                    const double2 c = psi[psi_slot((int)(k & (N - 1)))];
-#endif
-                    const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
-                    bre[h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
-                    bim[h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
-                } else {
-                    const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
-                    fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h][bb], bim[h][bb]);
-                }
-            }
+        // latency shape: computed at the top of the step (the lookups' LDS latency hides
+        // behind the digits and the forward FFT); throughput shapes: here (VGPR budget)
+        if constexpr (!LAT) psi_factors();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             double2 Bn[3][2];
