@@ -1,6 +1,8 @@
 // extern "C" boundary (include/fheregex.h): context, keys, ciphertext handles,
 // eager gate ops (the smart_* replacements), the batched has_match engine.
 #include <chrono>
+#include <climits>
+#include <cstdlib>
 #include <map>
 #include <cstring>
 #include <memory>
@@ -63,6 +65,8 @@ static double now_ms() {
 
 using namespace fr;
 
+struct fr_plan_cache;  // cached match plans (below)
+
 struct fr_ctx {
     Params p;
     std::unique_ptr<Device> dev;
@@ -78,6 +82,13 @@ struct fr_ctx {
     int keygen = FR_KEYGEN_AUTO;
     bool sk_on_device = false;  // server key generated on the device (export downloads it)
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
+    fr_plan_cache* plans = nullptr;
+
+    fr_ctx();
+    ~fr_ctx();
+    fr_ctx(const fr_ctx&) = delete;
+    fr_ctx& operator=(const fr_ctx&) = delete;
+    void clear_plans();
 
     Device& device() {
         if (!dev) throw Error(FR_ERR_NO_DEVICE, "host-only context: no HIP device");
@@ -115,34 +126,70 @@ namespace fr {
 constexpr int MV_MAX_NORM2 = 8;
 
 // ---------------------------------------------------------------- executor
-// Runs a PBS program whose negative sources refer to blocks of `inputs`
-// (input q = pos q: src = -(1 + q*4 + blk)).  Returns one slot per gate
-// (caller owns those slots).
-static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs,
-                                      fr_match_stats* st) {
+// A PBS program whose negative sources refer to blocks of `inputs` (input q =
+// pos q: src = -(1 + q*4 + blk)) compiles to a Plan: one DevGate batch per
+// dependency level, every input resolved to an arena slot (trivial blocks folded
+// into the offset), small-norm LUTs on the same linear combination merged into one
+// multi-value rotation.  Every gate is validated before any slot is allocated, and
+// the slots allocated so far are returned if compilation throws.
+struct Plan {
+    std::vector<DevGate> gates;     // levels concatenated
+    std::vector<size_t> level_off;  // level l (0-based): gates [level_off[l], level_off[l+1])
+    std::vector<int> slot;          // output slot per program gate
+    uint64_t pbs = 0, rotations = 0, levels = 0, max_width = 0;
+    DevGate* d_gates = nullptr;     // device-resident copy (cached plans)
+};
+
+static void free_plan_slots(Device& dev, std::vector<int>& slot) {
+    for (int& s : slot)
+        if (s >= 0) dev.free_slot(s), s = -1;
+}
+
+static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs) {
     Device& dev = ctx->device();
     if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
-    std::vector<int> slot(gates.size(), -1);
+    // 1. validation (no allocation): topological order, input range, fan-in, offsets
     std::vector<int> level(gates.size(), 0);
     int maxl = 0;
     for (size_t g = 0; g < gates.size(); ++g) {
-        int l = 0;
-        for (auto& in : gates[g].ins)
+        const PGate& G = gates[g];
+        int l = 0, nin = 0, off = G.offset;
+        for (auto& in : G.ins) {
             if (in.src >= 0) {
                 if ((size_t)in.src >= g) throw Error(FR_ERR_INVALID, "gate program is not topologically ordered");
                 l = std::max(l, level[in.src]);
+                ++nin;
+                continue;
             }
+            const int cb = -in.src - 1;
+            const size_t q = (size_t)(cb / 4);
+            if (q >= inputs.size()) throw Error(FR_ERR_INVALID, "gate input out of range");
+            const Block& b = ctx->get(inputs[q]).b[cb % 4];
+            if (b.slot < 0) off += 2 * in.w * (int)b.triv;
+            else ++nin;
+        }
+        if (nin > 16) throw Error(FR_ERR_INVALID, "gate fan-in > 16");
+        if (G.kind != GATE_SIGN && (off & 1)) throw Error(FR_ERR_INVALID, "LUT gate with a half-integral offset");
         level[g] = l + 1;
         maxl = std::max(maxl, l + 1);
     }
     std::vector<std::vector<int>> by_level(maxl + 1);
     for (size_t g = 0; g < gates.size(); ++g) by_level[level[g]].push_back((int)g);
-    for (size_t g = 0; g < gates.size(); ++g) slot[g] = dev.alloc_slot();
-    std::vector<DevGate> batch;
-    size_t maxw = 0;
-    uint64_t jobs = 0;
+    // 2. allocation and batches
+    Plan P;
+    P.slot.assign(gates.size(), -1);
+    struct Guard {
+        Device& dev;
+        std::vector<int>& slot;
+        bool armed = true;
+        ~Guard() {
+            if (armed) free_plan_slots(dev, slot);
+        }
+    } guard{dev, P.slot};
+    for (size_t g = 0; g < gates.size(); ++g) P.slot[g] = dev.alloc_slot();
+    P.level_off.push_back(0);
     for (int l = 1; l <= maxl; ++l) {
-        batch.clear();
+        const size_t first = P.gates.size();
         // input signature -> open job index (multi-value bootstrapping merges
         // small-norm LUTs that read the same linear combination)
         std::map<std::vector<int32_t>, size_t> open_job;
@@ -150,25 +197,20 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
             const PGate& G = gates[g];
             DevGate d;
             std::memset(&d, 0, sizeof d);
-            int off = G.offset;
-            int nin = 0;
+            int off = G.offset, nin = 0;
             for (auto& in : G.ins) {
                 int s;
                 if (in.src >= 0) {
-                    s = slot[in.src];
+                    s = P.slot[in.src];
                 } else {
-                    int cb = -in.src - 1;
-                    size_t q = (size_t)(cb / 4);
-                    if (q >= inputs.size()) throw Error(FR_ERR_INVALID, "gate input out of range");
-                    const HandleRec& h = ctx->get(inputs[q]);
-                    const Block& b = h.b[cb % 4];
+                    const int cb = -in.src - 1;
+                    const Block& b = ctx->get(inputs[(size_t)(cb / 4)]).b[cb % 4];
                     if (b.slot < 0) {
                         off += 2 * in.w * (int)b.triv;  // offsets are in units of Delta/2
                         continue;
                     }
                     s = b.slot;
                 }
-                if (nin >= 16) throw Error(FR_ERR_INVALID, "gate fan-in > 16");
                 d.in_slot[nin] = s;
                 d.in_w[nin] = in.w;
                 ++nin;
@@ -178,11 +220,10 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
             if (G.kind == GATE_SIGN) {
                 d.n_out = 1;
                 d.direct = JOB_SIGN;
-                d.out_slot[0] = slot[g];
-                batch.push_back(d);
+                d.out_slot[0] = P.slot[g];
+                P.gates.push_back(d);
                 continue;
             }
-            if (off & 1) throw Error(FR_ERR_INVALID, "LUT gate with a half-integral offset");
             const bool small = lut_w_norm2(G.lut) <= MV_MAX_NORM2;
             if (small && ctx->multi_value) {
                 std::vector<int32_t> sig{nin, off};
@@ -191,90 +232,251 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
                     sig.push_back(d.in_w[q]);
                 }
                 auto it = open_job.find(sig);
-                if (it != open_job.end() && batch[it->second].n_out < MAX_OUT) {
-                    DevGate& J = batch[it->second];
+                if (it != open_job.end() && P.gates[it->second].n_out < MAX_OUT) {
+                    DevGate& J = P.gates[it->second];
                     std::memcpy(J.lut[J.n_out], G.lut, 16);
-                    J.out_slot[J.n_out] = slot[g];
+                    J.out_slot[J.n_out] = P.slot[g];
                     J.n_out++;
                     J.direct = JOB_MULTI;
                     continue;
                 }
-                open_job[sig] = batch.size();
+                open_job[sig] = P.gates.size();
             }
             std::memcpy(d.lut[0], G.lut, 16);
             d.n_out = 1;
             d.direct = JOB_DIRECT;
-            d.out_slot[0] = slot[g];
-            batch.push_back(d);
+            d.out_slot[0] = P.slot[g];
+            P.gates.push_back(d);
         }
-        maxw = std::max(maxw, batch.size());
-        jobs += batch.size();
-        dev.run_level(batch.data(), batch.size());
+        P.level_off.push_back(P.gates.size());
+        P.max_width = std::max<uint64_t>(P.max_width, P.gates.size() - first);
     }
-    if (st) {
-        st->pbs += gates.size();
-        st->blind_rotations += jobs;
-        st->levels += (uint64_t)maxl;
-        st->max_level_width = std::max<uint64_t>(st->max_level_width, maxw);
-    }
-    return slot;
+    P.pbs = gates.size();
+    P.rotations = P.gates.size();
+    P.levels = (uint64_t)maxl;
+    guard.armed = false;
+    return P;
 }
 
-// result handle of a program: boolean from a gate slot, maybe negated, or trivial
-static fr_ct finish_output(fr_ctx* ctx, const Program& prog, std::vector<int>& slots) {
+// enqueue every level of a plan (async on the device stream)
+static void launch_plan(Device& dev, const Plan& P) {
+    for (size_t l = 0; l + 1 < P.level_off.size(); ++l) {
+        const size_t a = P.level_off[l], n = P.level_off[l + 1] - a;
+        if (P.d_gates) dev.run_level_resident(P.d_gates + a, P.gates.data() + a, n);
+        else dev.run_level(P.gates.data() + a, n);
+    }
+}
+
+static void add_plan_stats(const Plan& P, fr_match_stats* st) {
+    if (!st) return;
+    st->pbs += P.pbs;
+    st->blind_rotations += P.rotations;
+    st->levels += P.levels;
+    st->max_level_width = std::max<uint64_t>(st->max_level_width, P.max_width);
+}
+
+// Runs a program and returns one slot per gate (the caller owns those slots).
+static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs,
+                                      fr_match_stats* st) {
+    Plan P = compile_plan(ctx, gates, inputs);
+    launch_plan(ctx->device(), P);
+    add_plan_stats(P, st);
+    return std::move(P.slot);
+}
+
+// result handle of a program: boolean out_const + out_w * gate slot (a linear
+// op, no bootstrap), or trivial.  take_slot: the output gate's slot becomes the
+// result's (else the result is a fresh slot and `slots` stay untouched).
+static fr_ct finish_output(fr_ctx* ctx, int out_gate, int out_w, int out_const, std::vector<int>& slots,
+                           bool take_slot) {
     HandleRec r;
     r.is_bool = true;
-    if (prog.out_gate < 0) {
-        r.b[0].triv = (uint8_t)prog.out_const;
-    } else if (prog.out_w == 1 && prog.out_const == 0) {
-        r.b[0].slot = slots[prog.out_gate];
-        slots[prog.out_gate] = -1;
+    if (out_gate < 0) {
+        r.b[0].triv = (uint8_t)out_const;
+    } else if (take_slot && out_w == 1 && out_const == 0) {
+        r.b[0].slot = slots[out_gate];
+        slots[out_gate] = -1;
     } else {
         DevGate d;
         std::memset(&d, 0, sizeof d);
         d.n_in = 1;
-        d.in_slot[0] = slots[prog.out_gate];
-        d.in_w[0] = prog.out_w;
-        d.offset = 2 * prog.out_const;
+        d.in_slot[0] = slots[out_gate];
+        d.in_w[0] = out_w;
+        d.offset = 2 * out_const;
         d.out_slot[0] = ctx->device().alloc_slot();
         ctx->device().run_linear(d);
         r.b[0].slot = d.out_slot[0];
     }
-    for (int s : slots)
-        if (s >= 0) ctx->device().free_slot(s);
+    if (take_slot) free_plan_slots(ctx->device(), slots);
     ctx->device().sync();
     return ctx->new_handle(r);
 }
 
 static fr_ct run_program(fr_ctx* ctx, const Program& prog, const std::vector<fr_ct>& inputs, fr_match_stats* st) {
     std::vector<int> slots = execute_gates(ctx, prog.gates, inputs, st);
-    return finish_output(ctx, prog, slots);
+    return finish_output(ctx, prog.out_gate, prog.out_w, prog.out_const, slots, true);
 }
 
 static int cblk(int pos, int blk) { return -(1 + pos * 4 + blk); }
 
+// ------------------------------------------------------------ plan cache
+// The circuit of a match is data-oblivious: the same (pattern, grammar, engine,
+// lowering, multi-value, length, start range) and the same content slots give
+// the same plan.  A cached plan keeps its intermediate slots and a device copy
+// of its gate batches, so a repeat call skips parse -> record -> lower ->
+// compile and the per-level descriptor uploads: it only enqueues the levels.
+struct CachedMatch {
+    std::string key;
+    std::vector<int32_t> sig;  // per content position and block: slot, -1 - trivial value, or absent / bool markers
+    Plan plan;
+    int32_t out_gate = -1, out_w = 0, out_const = 0;
+    uint64_t ct_ops = 0, cache_hits = 0, n_branches = 0;
+    uint64_t last_use = 0;
+};
+
+}  // namespace fr
+
+struct fr_plan_cache {
+    std::vector<std::unique_ptr<fr::CachedMatch>> entries;
+    size_t capacity = 8;
+    uint64_t clock = 0, hits = 0, misses = 0;
+};
+
+namespace fr {
+
+static void drop_cached(fr_ctx* ctx, CachedMatch& e);
+
+static std::string match_key(fr_ctx* ctx, const char* pattern, size_t n, size_t lo, size_t hi) {
+    std::string k = std::to_string(ctx->grammar) + "|" + std::to_string(ctx->engine) + "|" +
+                    std::to_string(ctx->lowering) + "|" + std::to_string((int)ctx->multi_value) + "|" +
+                    std::to_string(n) + "|" + std::to_string(lo) + "|" + std::to_string(hi) + "|";
+    k += pattern;
+    return k;
+}
+static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content, size_t n) {
+    constexpr int32_t ABSENT = INT32_MIN, BOOL = INT32_MIN + 1;
+    std::vector<int32_t> sig;
+    sig.reserve(4 * n);
+    for (size_t q = 0; q < n; ++q) {
+        if (content[q] == 0xFFFFFFFFu) {
+            sig.insert(sig.end(), 4, ABSENT);
+            continue;
+        }
+        const HandleRec& h = ctx->get(content[q]);
+        for (int b = 0; b < 4; ++b) sig.push_back(h.is_bool ? BOOL : h.b[b].slot >= 0 ? h.b[b].slot : -1 - (int32_t)h.b[b].triv);
+    }
+    return sig;
+}
+
+}  // namespace fr
+
+fr_ctx::fr_ctx() : plans(new fr_plan_cache) {
+    if (const char* ev = std::getenv("FR_PLAN_CACHE")) plans->capacity = (size_t)std::max(0, std::atoi(ev));
+}
+void fr_ctx::clear_plans() {
+    if (!plans) return;
+    for (auto& e : plans->entries) fr::drop_cached(this, *e);
+    plans->entries.clear();
+}
+fr_ctx::~fr_ctx() {
+    try {
+        clear_plans();
+    } catch (...) {
+    }
+    delete plans;
+}
+
+namespace fr {
+
+static void drop_cached(fr_ctx* ctx, CachedMatch& e) {
+    if (!ctx->dev) return;
+    ctx->dev->sync();  // no level of this plan may still be in flight
+    free_plan_slots(*ctx->dev, e.plan.slot);
+    ctx->dev->free_gates(e.plan.d_gates);
+    e.plan.d_gates = nullptr;
+}
 
 static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
                         fr_match_stats* st) {
     double t0 = now_ms();
-    ValueDag dag;
-    GrammarScope grammar(ctx->grammar);
-    Recorded rec = record_has_match_engine(dag, n, pattern ? pattern : "", lo, hi, ctx->engine);
-    Program prog = lower(dag, rec.root, ctx->lowering);
-    double t1 = now_ms();
-    std::vector<fr_ct> inputs(content, content + n);
-    // validate referenced content handles
-    for (auto& g : prog.gates)
-        for (auto& in : g.ins)
-            if (in.src < 0) {
-                size_t q = (size_t)((-in.src - 1) / 4);
-                if (q >= n || content[q] == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
-                const HandleRec& h = ctx->get(content[q]);
-                if (h.is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
-            }
-    DeviceTimers before = ctx->device().timers();
+    pattern = pattern ? pattern : "";
+    Device& dev = ctx->device();
+    if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
+    fr_plan_cache& pc = *ctx->plans;
+    CachedMatch* hit = nullptr;
+    std::string key;
+    std::vector<int32_t> sig;
+    if (pc.capacity) {
+        key = match_key(ctx, pattern, n, lo, hi);
+        sig = content_signature(ctx, content, n);
+        for (auto& e : pc.entries)
+            if (e->key == key && e->sig == sig) hit = e.get();
+    }
     fr_match_stats local{};
-    fr_ct out = run_program(ctx, prog, inputs, &local);
+    Recorded rec;
+    bool cached = hit != nullptr;
+    double t1;
+    DeviceTimers before = dev.timers();
+    fr_ct out;
+    if (hit) {
+        ++pc.hits;
+        hit->last_use = ++pc.clock;
+        t1 = now_ms();
+        launch_plan(dev, hit->plan);
+        add_plan_stats(hit->plan, &local);
+        rec.ct_ops = hit->ct_ops;
+        rec.cache_hits = hit->cache_hits;
+        rec.n_branches = hit->n_branches;
+        out = finish_output(ctx, hit->out_gate, hit->out_w, hit->out_const, hit->plan.slot, false);
+    } else {
+        ++pc.misses;
+        ValueDag dag;
+        GrammarScope grammar(ctx->grammar);
+        rec = record_has_match_engine(dag, n, pattern, lo, hi, ctx->engine);
+        Program prog = lower(dag, rec.root, ctx->lowering);
+        // validate referenced content handles
+        for (auto& g : prog.gates)
+            for (auto& in : g.ins)
+                if (in.src < 0) {
+                    size_t q = (size_t)((-in.src - 1) / 4);
+                    if (q >= n || content[q] == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
+                    const HandleRec& h = ctx->get(content[q]);
+                    if (h.is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
+                }
+        std::vector<fr_ct> inputs(content, content + n);
+        Plan P = compile_plan(ctx, prog.gates, inputs);
+        t1 = now_ms();
+        add_plan_stats(P, &local);
+        if (pc.capacity && !P.gates.empty()) {
+            // keep the plan: its slots stay allocated, its batches go to the device once
+            auto e = std::make_unique<CachedMatch>();
+            e->key = std::move(key);
+            e->sig = std::move(sig);
+            e->out_gate = prog.out_gate;
+            e->out_w = prog.out_w;
+            e->out_const = prog.out_const;
+            e->ct_ops = rec.ct_ops;
+            e->cache_hits = rec.cache_hits;
+            e->n_branches = rec.n_branches;
+            e->last_use = ++pc.clock;
+            e->plan = std::move(P);
+            e->plan.d_gates = dev.upload_gates(e->plan.gates.data(), e->plan.gates.size());
+            if (pc.entries.size() >= pc.capacity) {  // evict the least recently used
+                size_t v = 0;
+                for (size_t i = 1; i < pc.entries.size(); ++i)
+                    if (pc.entries[i]->last_use < pc.entries[v]->last_use) v = i;
+                drop_cached(ctx, *pc.entries[v]);
+                pc.entries.erase(pc.entries.begin() + (long)v);
+            }
+            CachedMatch& c = *e;
+            pc.entries.push_back(std::move(e));
+            launch_plan(dev, c.plan);
+            out = finish_output(ctx, c.out_gate, c.out_w, c.out_const, c.plan.slot, false);
+        } else {
+            launch_plan(dev, P);
+            out = finish_output(ctx, prog.out_gate, prog.out_w, prog.out_const, P.slot, true);
+        }
+    }
     double t2 = now_ms();
     if (st) {
         std::memset(st, 0, sizeof *st);
@@ -287,7 +489,8 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
         st->max_level_width = local.max_level_width;
         st->host_ms = t1 - t0;
         st->device_ms = t2 - t1;
-        const DeviceTimers& after = ctx->device().timers();
+        st->plan_cached = cached ? 1 : 0;
+        const DeviceTimers& after = dev.timers();
         st->br_kernel_ms = after.br_ms - before.br_ms;
         st->ks_kernel_ms = after.ks_ms - before.ks_ms;
         st->br_launches = after.br_launches - before.br_launches;
@@ -611,7 +814,10 @@ int fr_radix_deserialize(fr_ctx* ctx, const uint8_t* buf, size_t len, uint64_t* 
             if (off + 8 * L > len) throw Error(FR_ERR_INVALID, "radix ciphertext: truncated");
             std::memcpy(blocks + b * L, buf + off, 8 * L);
             off += 8 * L;
-            (void)get();  // degree
+            // the comparison LUTs read clean 2-bit blocks (x0 + 4 x1 in [0, 16)); a block
+            // carrying a carry (degree > message_modulus - 1) would decode silently wrong
+            if (get() > MESSAGE_MODULUS - 1)
+                throw Error(FR_ERR_INVALID, "radix ciphertext: block degree exceeds message_modulus - 1 (carries not propagated)");
             if (get() != MESSAGE_MODULUS || get() != CARRY_MODULUS)
                 throw Error(FR_ERR_INVALID, "radix ciphertext: message/carry modulus does not match the parameters");
         }
@@ -906,6 +1112,21 @@ int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n, const char* patter
     FR_TRY({
         NEED(ctx && out && pattern && (content || !n));
         *out = match_impl(ctx, content, n, pattern, 0, n, st);
+    })
+}
+
+int fr_set_plan_cache(fr_ctx* ctx, size_t capacity) {
+    FR_TRY({
+        NEED(ctx);
+        auto& pc = *ctx->plans;
+        pc.capacity = capacity;
+        while (pc.entries.size() > capacity) {  // drop the least recently used beyond the new capacity
+            size_t v = 0;
+            for (size_t i = 1; i < pc.entries.size(); ++i)
+                if (pc.entries[i]->last_use < pc.entries[v]->last_use) v = i;
+            drop_cached(ctx, *pc.entries[v]);
+            pc.entries.erase(pc.entries.begin() + (long)v);
+        }
     })
 }
 

@@ -70,6 +70,11 @@ class Device {
 
     // run one dependency level of gates (all independent), async on the stream
     void run_level(const DevGate* gates, size_t n);
+    // the same for a batch already resident on the device (upload_gates); `host`
+    // is its host copy (validated when uploaded; read for the profiling counters)
+    void run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n);
+    DevGate* upload_gates(const DevGate* gates, size_t n);  // validated, synchronous
+    void free_gates(DevGate* d);                            // after the stream drained
     // linear combination without bootstrap (NOT of a boolean): out = offset*2^58 + sum w*in
     void run_linear(const DevGate& g);
     void sync();
@@ -95,6 +100,8 @@ class Device {
     // its previous H2D copy completed (no stream-wide sync between levels)
     DevGate* stage_acquire();
     void stage_copy(size_t n);
+    void validate_gates(const DevGate* gates, size_t n) const;
+    void launch_level(const DevGate* d_gates, const DevGate* host, size_t n);
     // profiling: per-level event triples resolved at sync() (no sync per level)
     void* take_event();
     void resolve_timers();

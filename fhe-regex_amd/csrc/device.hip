@@ -784,19 +784,27 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
 
-// lincomb + digits: one thread per (gate, input coefficient); the body per gate
+// lincomb + digits: one thread per (gate, input coefficient); the body per gate.
+// The same launch zeroes the mask words of each output row (the MFMA pass
+// subtracts into them with atomics) and the padding digit rows B <= g < gridDim.y.
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
 k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride, int big,
-            int8_t* __restrict__ dig, uint64_t* __restrict__ body, int body_stride) {
+            int8_t* __restrict__ dig, uint64_t* __restrict__ ks, int ks_n, int ks_stride) {
     const int g = blockIdx.y;
+    if (g >= B) {  // padding row of the last 32-row tile: zero digits
+        int4* o = (int4*)(dig + (size_t)g * big * KSL);
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < big * KSL / 16; i += gridDim.x * 256) o[i] = int4{0, 0, 0, 0};
+        return;
+    }
     const DevGate& gg = gates[g];
     const int nin = gg.n_in;
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < ks_n; t += gridDim.x * 256) ks[(size_t)g * ks_stride + t] = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i <= big; i += gridDim.x * 256) {
         uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
         for (int q = 0; q < nin; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i];
         if (i == big) {
-            body[(size_t)g * body_stride] = v;  // column n of the (zeroed) output row; the MFMA pass subtracts
+            ks[(size_t)g * ks_stride + ks_n] = v;  // column n of the output row; the MFMA pass subtracts
         } else {
             int32_t d[KSL];
             ks_decompose<KSB, KSL>(v, d);
@@ -1160,10 +1168,9 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         const int MR = n >= ks_mr4_min_ ? 4 : 1;  // row tiles per wave
         const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
-        if (bp > n) HIP_CHECK(hipMemsetAsync(d_dig_ + n * KD, 0, (bp - n) * KD, STREAM));
-        HIP_CHECK(hipMemsetAsync(d_ks, 0, (size_t)8 * p_.ks_stride() * n, STREAM));
-        k_ks_digits<3, 5><<<dim3(8, (unsigned)n), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
-                                                                     p_.big(), d_dig_, d_ks + p_.n, p_.ks_stride());
+        if (KD % 16) throw Error(FR_ERR_INVALID, "MFMA keyswitch: digit rows must be whole 16-byte vectors");
+        k_ks_digits<3, 5><<<dim3(8, (unsigned)bp), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
+                                                                      p_.big(), d_dig_, d_ks, p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         // column tiles per wave (A-fragment reuse; auto: two from 512 gates, where the
         // traffic of re-read digit rows dominates: 178 -> 157 us at 512, 609 -> 472 us at 2048)
@@ -1216,9 +1223,7 @@ void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
     HIP_CHECK(hipGetLastError());
 }
 
-void Device::run_level(const DevGate* gates, size_t n) {
-    if (!n) return;
-    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+void Device::validate_gates(const DevGate* gates, size_t n) const {
     for (size_t i = 0; i < n; ++i) {
         const DevGate& g = gates[i];
         if (g.n_in < 0 || g.n_in > 16 || g.n_out < 1 || g.n_out > MAX_OUT || g.direct < 0 || g.direct > 2 ||
@@ -1229,24 +1234,55 @@ void Device::run_level(const DevGate* gates, size_t n) {
         for (int q = 0; q < g.n_in; ++q)
             if (g.in_slot[q] < 0 || (size_t)g.in_slot[q] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad input slot");
     }
+}
+
+void Device::run_level(const DevGate* gates, size_t n) {
+    if (!n) return;
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    validate_gates(gates, n);
     ensure_batch(n);
     // d_gates_ / d_ks_ are reused in stream order (this level's copy runs after
     // the previous level's kernels); only the host staging buffer needs a wait
     std::memcpy(stage_acquire(), gates, sizeof(DevGate) * n);
     stage_copy(n);
+    launch_level(d_gates_, gates, n);
+}
+
+void Device::run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n) {
+    if (!n) return;
+    if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    ensure_batch(n);
+    launch_level(d_gates, host, n);
+}
+
+DevGate* Device::upload_gates(const DevGate* gates, size_t n) {
+    validate_gates(gates, n);
+    DevGate* d = nullptr;
+    HIP_CHECK(hipMalloc(&d, sizeof(DevGate) * std::max<size_t>(n, 1)));
+    HIP_CHECK(hipMemcpy(d, gates, sizeof(DevGate) * n, hipMemcpyHostToDevice));
+    return d;
+}
+
+void Device::free_gates(DevGate* d) {
+    if (!d) return;
+    HIP_CHECK(hipStreamSynchronize(STREAM));
+    HIP_CHECK(hipFree(d));
+}
+
+void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n) {
     PendingTimer t{};
     if (profiling_) {
         for (auto& e : t.ev) e = take_event();
         HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[0], STREAM));
     }
-    launch_ks(d_gates_, n, d_ks_);
+    launch_ks(d_gates, n, d_ks_);
     if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[1], STREAM));
-    launch_br(d_gates_, d_ks_, n);
+    launch_br(d_gates, d_ks_, n);
     if (profiling_) {
         HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[2], STREAM));
         t.gates = n;
         t.outs = 0;
-        for (size_t i = 0; i < n; ++i) t.outs += gates[i].n_out;
+        for (size_t i = 0; i < n; ++i) t.outs += host[i].n_out;
         pending_.push_back(t);
     }
 }

@@ -66,7 +66,8 @@ class MatchStats(C.Structure):
     _fields_ = [("ct_ops", C.c_uint64), ("cache_hits", C.c_uint64), ("n_branches", C.c_uint64),
                 ("pbs", C.c_uint64), ("blind_rotations", C.c_uint64), ("levels", C.c_uint64), ("max_level_width", C.c_uint64),
                 ("host_ms", C.c_double), ("device_ms", C.c_double), ("br_kernel_ms", C.c_double),
-                ("ks_kernel_ms", C.c_double), ("br_launches", C.c_uint64), ("br_gates", C.c_uint64)]
+                ("ks_kernel_ms", C.c_double), ("br_launches", C.c_uint64), ("br_gates", C.c_uint64),
+                ("plan_cached", C.c_uint64)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}
@@ -129,6 +130,7 @@ _SIGS = {
     "fr_has_match_range": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t,
                                      C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
+    "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_engine": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_set_grammar": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_parse_ex": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_size_t]),
@@ -284,6 +286,10 @@ class Context:
 
     def set_multi_value(self, on: bool):
         _check(lib().fr_set_multi_value(self.h, int(on)))
+
+    def set_plan_cache(self, capacity: int):
+        """Plans kept for repeat has_match calls (0: off, frees the cached plans)."""
+        _check(lib().fr_set_plan_cache(self.h, capacity))
 
     def set_profiling(self, on: bool):
         _check(lib().fr_set_profiling(self.h, int(on)))

@@ -87,12 +87,13 @@ typedef struct {
     uint64_t blind_rotations; /* blind rotations (several LUTs may share one: multi-value bootstrapping) */
     uint64_t levels;        /* dependent PBS levels (launch batches) */
     uint64_t max_level_width;
-    double host_ms;         /* parse + enumerate + record + lower */
+    double host_ms;         /* parse + enumerate + record + lower + compile (plan-cache hit: the lookup) */
     double device_ms;       /* device execution, wall */
     double br_kernel_ms;    /* sum of blind-rotation kernel durations (HIP events) */
     double ks_kernel_ms;    /* sum of lincomb+keyswitch kernel durations (HIP events) */
     uint64_t br_launches;
     uint64_t br_gates;      /* bootstraps across all blind-rotation launches */
+    uint64_t plan_cached;   /* 1: the match replayed a cached plan (fr_set_plan_cache) */
 } fr_match_stats;
 
 /* ----- context ----- */
@@ -192,6 +193,12 @@ int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* 
                  fr_match_stats* stats);
 /* Same, restricted to start offsets [start_lo, start_hi) — the per-GPU shard of
  * the start-offset partition (the OR over shards equals has_match). */
+/* Plan cache: has_match circuits are data-oblivious, so the lowered, compiled
+ * plan of (pattern, grammar, engine, lowering, multi-value, n_chars, start range,
+ * content slots) is kept -- its intermediate slots and its device-resident gate
+ * batches -- and a repeat call only enqueues its levels.  capacity = plans kept
+ * (LRU; default 8, env FR_PLAN_CACHE); 0 disables and frees every cached plan. */
+int fr_set_plan_cache(fr_ctx* ctx, size_t capacity);
 int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
                        size_t start_hi, fr_ct* out, fr_match_stats* stats);
 

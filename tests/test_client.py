@@ -52,6 +52,12 @@ def test_wire_rejects_malformed(hctx):
     struct.pack_into("<Q", bad, 0, 1 << 40)
     with pytest.raises(F.FheRegexError):
         hctx.deserialize_radix(bytes(bad))
+    # a block with carries (degree > message_modulus - 1) is refused, not decoded wrong
+    bad = bytearray(data)
+    struct.pack_into("<Q", bad, 16 + 8 * hctx.lwe_len, 4)
+    with pytest.raises(F.FheRegexError, match="degree"):
+        hctx.deserialize_radix(bytes(bad))
+    assert hctx.serialize_radix(hctx.encrypt_str("a", seed=1)[0], degree=3)  # clean blocks still accepted
 
 
 def test_device_encryption_needs_device(hctx):

@@ -337,6 +337,40 @@ def test_start_range_shards_or_to_full(gctx):
     assert gctx.decrypt_radix(gctx.download_radix(gctx.or_many(parts))) == 1
 
 
+def test_plan_cache_replays_bit_identical(gctx):
+    """A repeat has_match replays the cached plan: same output ciphertext words,
+    same counters, no host lowering; other content slots or settings miss."""
+    rng = np.random.default_rng(11)
+    s = _printable(rng, 48)
+    s = s[:30] + "abc" + s[33:]
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=12))
+    o1, st1 = gctx.has_match(hs, "/abc/")
+    o2, st2 = gctx.has_match(hs, "/abc/")
+    assert st2.plan_cached == 1
+    assert (st1.ct_ops, st1.pbs, st1.blind_rotations, st1.levels) == (st2.ct_ops, st2.pbs, st2.blind_rotations, st2.levels)
+    w1, w2 = gctx.download_radix(o1), gctx.download_radix(o2)
+    assert np.array_equal(w1, w2) and gctx.decrypt_radix(w2) == 1
+    # another range of starts, and other content handles (other slots): misses
+    o3, st3 = gctx.has_match(hs, "/abc/", 0, 20)
+    assert st3.plan_cached == 0 and gctx.decrypt_radix(gctx.download_radix(o3)) == 0
+    hs2 = gctx.upload_radix(gctx.encrypt_str(s[:30] + "xyz" + s[33:], seed=13))
+    o4, st4 = gctx.has_match(hs2, "/abc/")
+    assert st4.plan_cached == 0 and gctx.decrypt_radix(gctx.download_radix(o4)) == 0
+    o5, st5 = gctx.has_match(hs2, "/abc/")
+    assert st5.plan_cached == 1 and np.array_equal(gctx.download_radix(o4), gctx.download_radix(o5))
+    # the first plan is still cached and still reads its own slots
+    o6, st6 = gctx.has_match(hs, "/abc/")
+    assert st6.plan_cached == 1 and np.array_equal(gctx.download_radix(o6), w1)
+    gctx.set_plan_cache(0)
+    try:
+        o7, st7 = gctx.has_match(hs, "/abc/")
+        assert st7.plan_cached == 0 and np.array_equal(gctx.download_radix(o7), w1)
+    finally:
+        gctx.set_plan_cache(8)
+    for h in hs + hs2 + [o1, o2, o3, o4, o5, o6, o7]:
+        gctx.release(h)
+
+
 def test_k2_n1024_params(key_blob, fixture_key):
     """The N=1024 variant: the same 2048-bit key read as k=2 polynomials of 1024."""
     params = F.default_params(k=2, N=1024)
