@@ -44,7 +44,8 @@ void validate_params(const Params& p) {
     if (p.pbs_base_log != 23 || p.pbs_level != 1) throw Error(FR_ERR_INVALID, "only the 2^23 x 1 PBS gadget is supported");
     if (p.ks_base_log < 1 || p.ks_base_log * p.ks_level > 63) throw Error(FR_ERR_INVALID, "invalid keyswitch gadget");
     if (p.ring != FR_RING_RNS && p.ring != FR_RING_FFT) throw Error(FR_ERR_INVALID, "invalid ring");
-    if (p.ring == FR_RING_FFT && p.k != 1) throw Error(FR_ERR_INVALID, "the FFT ring is built for k = 1");
+    if (p.ring == FR_RING_FFT && !((p.k == 1 && p.N == 2048) || (p.k == 2 && p.N == 1024)))
+        throw Error(FR_ERR_INVALID, "the FFT ring is built for (k, N) = (1, 2048) and (2, 1024)");
 }
 
 struct Block {

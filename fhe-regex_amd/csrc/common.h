@@ -58,7 +58,7 @@ struct Params {
     int k = 1, N = 2048, n = 742;
     int ks_base_log = 3, ks_level = 5;
     int pbs_base_log = 23, pbs_level = 1;
-    int ring = FR_RING_FFT;  // blind-rotation ring (fheregex.h); k > 1 needs FR_RING_RNS
+    int ring = FR_RING_FFT;  // blind-rotation ring (fheregex.h)
     double lwe_sigma = 7.069849454709433e-06;
     double glwe_sigma = 2.9403601535432533e-16;
     int big() const { return k * N; }
@@ -67,9 +67,10 @@ struct Params {
     int slot_stride() const { return (lwe_len() + 7) & ~7; }
     int ks_stride() const { return (n + 1 + 7) & ~7; }
     int log2N() const { int l = 0; while ((1 << l) < N) ++l; return l; }
-    // bootstrapping-key unrolling: k = 1 processes LWE coefficients in pairs
-    // (3 GGSWs per pair: s_i s_j, s_i(1-s_j), (1-s_i)s_j); k > 1 one GGSW each
-    int bsk_unroll() const { return k == 1 ? 2 : 1; }
+    // bootstrapping-key unrolling: LWE coefficients in pairs (3 GGSWs per pair:
+    // s_i s_j, s_i(1-s_j), (1-s_i)s_j) for k = 1 and on the FFT ring; the RNS
+    // ring at k > 1 keeps one GGSW per coefficient
+    int bsk_unroll() const { return (k == 1 || ring == FR_RING_FFT) ? 2 : 1; }
     size_t bsk_ggsw() const { return bsk_unroll() == 2 ? 3 * (size_t)((n + 1) / 2) : (size_t)n; }
     size_t bsk_len() const { return bsk_ggsw() * (size_t)(k + 1) * (k + 1) * N; }
 };

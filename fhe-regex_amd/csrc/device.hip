@@ -925,7 +925,7 @@ static void set_smem_attr() {
 }
 
 static bool supported(const Params& p) {
-    if (p.ring == FR_RING_FFT) return p.N == 2048 && p.k == 1;
+    if (p.ring == FR_RING_FFT) return (p.N == 2048 && p.k == 1) || (p.N == 1024 && p.k == 2);
     return (p.N == 2048 && p.k == 1) || (p.N == 1024 && p.k == 2) || (p.N == 1024 && p.k == 1);
 }
 

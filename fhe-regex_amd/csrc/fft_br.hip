@@ -278,60 +278,50 @@ constexpr bool fexchanges_conflict_free() {
 // it: a transform's first cross-wave write follows the previous cross-wave
 // exchange's barrier, which every wave reaches only after its last read of the
 // other buffer; the inverse's first write (own slots) no longer meets the other
-// polynomial's MAC reads.
-template <int M, int E, int p, bool NOPRE>
-__device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
-    ffwd_phase<M, E, p>(x, tw, tl);
-    if constexpr (p + 1 < FGeo<M, E>::NPH) {
-        fexchange<M, E, p, p + 1, !NOPRE && ffwd_pre<M, E, p>()>(x, row, tl);
-        fforward_from<M, E, p + 1, NOPRE>(x, row, tw, tl);
-    }
-}
-template <int M, int E, int p, bool NOPRE>
-__device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const double2* tw, int tl) {
-    finv_phase<M, E, p>(x, tw, tl);
-    if constexpr (p > 0) {
-        fexchange<M, E, p, p - 1, !NOPRE && finv_pre<M, E, p>()>(x, row, tl);
-        finverse_from<M, E, p - 1, NOPRE>(x, row, tw, tl);
-    }
-}
-
-// the same with register twiddles (latency shape)
-// hook(integral_constant<p>) runs after phase p's butterflies (before its exchange)
-template <int M, int E, int p, class Hook>
-__device__ __forceinline__ void fforward_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr, int tl,
-                                                Hook&& hook) {
-    ffwd_phase_r<M, E, p>(x, twr);
+// polynomials' MAC reads.
+// TWR: twiddles from the lane's registers (twr), else from the LDS table tw.
+// hook(integral_constant<p>) runs after phase p's butterflies (before its exchange).
+template <int M, int E, int p, bool NOPRE, bool TWR, class Hook>
+__device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
+                                              const double2* tw, int tl, Hook&& hook) {
+    if constexpr (TWR) ffwd_phase_r<M, E, p>(x, twr);
+    else ffwd_phase<M, E, p>(x, tw, tl);
     hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
-        fexchange<M, E, p, p + 1, false>(x, row, tl);
-        fforward_from_r<M, E, p + 1>(x, row, twr, tl, hook);
+        fexchange<M, E, p, p + 1, !NOPRE && ffwd_pre<M, E, p>()>(x, row, tl);
+        fforward_from<M, E, p + 1, NOPRE, TWR>(x, row, twr, tw, tl, hook);
     }
 }
-template <int M, int E, int p>
-__device__ __forceinline__ void finverse_from_r(double2 (&x)[E], double2* row, const FTwr<M, E>& twr,
-                                                int tl) {
-    finv_phase_r<M, E, p>(x, twr);
+template <int M, int E, int p, bool NOPRE, bool TWR>
+__device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
+                                              const double2* tw, int tl) {
+    if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
+    else finv_phase<M, E, p>(x, tw, tl);
     if constexpr (p > 0) {
-        fexchange<M, E, p, p - 1, false>(x, row, tl);
-        finverse_from_r<M, E, p - 1>(x, row, twr, tl);
+        fexchange<M, E, p, p - 1, !NOPRE && finv_pre<M, E, p>()>(x, row, tl);
+        finverse_from<M, E, p - 1, NOPRE, TWR>(x, row, twr, tw, tl);
     }
 }
 
-template <int N, int E>
+// (K + 1) polynomials of M / E lanes each
+template <int N, int K, int E>
 constexpr int fbr_threads() {
-    return 2 * (N / 2 / E);
+    return (K + 1) * (N / 2 / E);
 }
 // Launch shapes (Device::launch_br_fft picks one by batch size):
-//  * latency, LAT (E = 4; launches of at most one bootstrap per CU): 8 waves,
-//    one workgroup per CU, 256 VGPRs; the step's 3 x 2 x E Fourier GGSW slots
-//    are loaded at the top of the step (they land during the digits and the
-//    forward FFT); the half psi^k table (k < N; psi^(k+N) = -psi^k) and two sets of exchange rows
-//    (forward + MAC / inverse: 3 barriers per step instead of 5) in LDS.
-//  * throughput (E = 4: 8 waves, 128 VGPRs; E = 8: 4 waves): two workgroups per
+//  * latency, LAT (E = 4; launches of at most one bootstrap per CU): one
+//    workgroup per CU (k = 1: 8 waves; k = 2, N = 1024: 6 waves), 256 VGPRs; the
+//    step's 3 x (k+1) x E Fourier GGSW slots are loaded at the top of the step
+//    (they land during the digits and the forward FFT); the half psi^k table
+//    (k < N; psi^(k+N) = -psi^k) and two sets of exchange rows (forward + MAC /
+//    inverse: 3 barriers per step instead of 5) in LDS.  k = 1 keeps the lane's
+//    twiddles in registers (TWR); k = 2 reads them from LDS (the 36 GGSW values
+//    take the registers).
+//  * throughput (k = 1, E = 4: 8 waves, 128 VGPRs; E = 8: 4 waves): two workgroups per
 //    CU (<= 80 KB of LDS each) hide each other's barriers and loads; a slot's
 //    GGSW values are loaded one slot ahead in the MAC; psi^k from the quadrant
-//    table (k < N/2) + quarter turns.
+//    table (k < N/2) + quarter turns.  k = 2, N = 1024: E = 8 is one wave per
+//    polynomial (every transform exchange wave-local), three workgroups per CU.
 // LDS slot of psi^k in the monomial table.  A lane's lookup index is k = e L mod 2N
 // with L = 1 + 4 brv(lane slot base), so the 16 lanes of a b128 read group share
 // k mod 32 (every lookup one bank quad: ~13-way conflicts).  Folding bits 5..9 into
@@ -339,23 +329,40 @@ constexpr int fbr_threads() {
 // blocks, so it serves the N-entry and the N/2-entry (quadrant) table alike.
 __device__ __forceinline__ int psi_slot(int k) { return k ^ ((k >> 6) & 15) ^ ((k >> 5) & 1); }
 
-template <int N, int E, bool LAT>
+template <int N, int K, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
-    return 16 * ((LAT ? 4 : 2) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 + (LAT ? (size_t)N : (size_t)N / 2)) +
+    return 16 * ((LAT ? 2 : 1) * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 +
+                 (LAT ? (size_t)N : (size_t)N / 2)) +
            16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT;
 }
-template <int E, bool LAT>
-constexpr int fbr_min_waves() {
-    return LAT ? 2 : (E == 4 ? 4 : 2);
+// workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
+template <int K, int E>
+constexpr int fbr_tp_groups() {
+    return K == 1 ? 2 : (E == 8 ? 3 : 2);
 }
-// the six Fourier GGSW values of slot m for this lane: [g][own row, other row]
-template <int M, int T>
-__device__ __forceinline__ void load_slot(double2 (&B)[3][2], const double2* bw, int P, int m, int tl) {
-    constexpr size_t GG = 4 * (size_t)M;
+// waves per SIMD the register allocation must allow
+template <int N, int K, int E, bool LAT>
+constexpr int fbr_min_waves() {
+    if (LAT) return 2;
+    if (K == 1) return E == 4 ? 4 : 2;
+    return E == 4 ? 3 : 2;  // k = 2: 2 x 6 waves (E = 4); E = 8: the one-slot-ahead loads need > 168 VGPRs
+}
+// row r != P of the MAC: the q-th other polynomial in ascending order
+template <int K>
+__device__ __forceinline__ int other_row(int P, int q) {
+    return q < P ? q : q + 1;
+}
+// the 3 (K+1) Fourier GGSW values of slot m for this lane: [g][own row, other rows...]
+// (Fourier GGSW [r][c][m][lane]: row r, output column c = P)
+template <int M, int T, int K>
+__device__ __forceinline__ void load_slot(double2 (&B)[3][K + 1], const double2* bw, int P, int m, int tl) {
+    constexpr size_t GG = (size_t)(K + 1) * (K + 1) * M;
 #pragma unroll
     for (int gg = 0; gg < 3; ++gg) {
-        B[gg][0] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
-        B[gg][1] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+        B[gg][0] = (bw + (size_t)gg * GG + (size_t)(P * (K + 1) + P) * M + (size_t)m * T)[tl];
+#pragma unroll
+        for (int q = 0; q < K; ++q)
+            B[gg][1 + q] = (bw + (size_t)gg * GG + (size_t)(other_row<K>(P, q) * (K + 1) + P) * M + (size_t)m * T)[tl];
     }
 }
 
@@ -385,20 +392,22 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
     return acc;
 }
 
-template <int N, int E, bool LAT>
-__global__ void __launch_bounds__((fbr_threads<N, E>()), (fbr_min_waves<E, LAT>()))
+template <int N, int K, int E, bool LAT>
+__global__ void __launch_bounds__((fbr_threads<N, K, E>()), (fbr_min_waves<N, K, E, LAT>()))
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
                    const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ psi_g,
                    const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena, int slot_stride) {
     constexpr int M = N / 2;
     using G = FGeo<M, E>;
     static_assert(fexchanges_conflict_free<M, E>(), "LDS maps must make every exchange conflict-free");
-    constexpr int T = M / E, NT = 2 * T, LAST = G::NPH - 1, XL = G::XL;
+    static_assert(!LAT || E == 4, "the latency shape holds a step's GGSW values in registers: E = 4");
+    constexpr int T = M / E, NT = (K + 1) * T, LAST = G::NPH - 1, XL = G::XL;
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
+    constexpr bool TWR = LAT && K == 1;  // twiddles in registers
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
-    double2* xbuf = fsm;                  // 2 rows of NP complex: row P at P * NP
-    double2* ibuf = LAT ? xbuf + 2 * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
-    double2* tw = xbuf + (LAT ? 4 : 2) * G::NP;     // M forward twiddles
+    double2* xbuf = fsm;                  // K+1 rows of NP complex: row P at P * NP
+    double2* ibuf = LAT ? xbuf + (K + 1) * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
+    double2* tw = xbuf + (LAT ? 2 : 1) * (K + 1) * G::NP;  // M forward twiddles
     constexpr int NPSI = LAT ? N : N / 2;
     double2* psi = tw + M;                // psi^k, k < NPSI
     uint8_t* lut = (uint8_t*)(psi + NPSI);             // 16 * n_out
@@ -418,16 +427,16 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
     const uint32_t bbar = mod_switch(in[n], LOG2N2);
-    // leaf exponents mod 1024 of this lane's slot bases (slots 4b): L(j) = 1 + 4 brv(j)
+    // leaf exponents mod M of this lane's slot bases (slots 4b): L(j) = 1 + 4 brv(j)
     // (fft::Tables::leaf, checked against the table in tests/test_fft.py)
     uint32_t Lb[E / 4];
 #pragma unroll
     for (int bb = 0; bb < E / 4; ++bb)
-        Lb[bb] = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 4 * bb)) >> (32 - G::LOG))) & 1023u;
+        Lb[bb] = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 4 * bb)) >> (32 - G::LOG))) & (uint32_t)(M - 1);
     __syncthreads();
 
     // accumulator (u64 torus), natural order: lane holds coefficients j and j + M
-    // for j = idx<0>(tl, m); mask polynomial 0, body X^-bbar * V
+    // for j = idx<0>(tl, m); mask polynomials 0, body (polynomial K) X^-bbar * V
     uint64_t alo[E], ahi[E];
     {
         const bool direct = kind == JOB_DIRECT;
@@ -441,24 +450,25 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut);
                 v[h] = s < N ? tv : (uint64_t)0 - tv;
             }
-            alo[m] = P == 1 ? v[0] : 0;
-            ahi[m] = P == 1 ? v[1] : 0;
+            alo[m] = P == K ? v[0] : 0;
+            ahi[m] = P == K ? v[1] : 0;
         }
     }
 
     double2* row = xbuf + P * G::NP;
     double2* irow = ibuf + P * G::NP;
-    const double2* orow = xbuf + (1 - P) * G::NP;
     const int bl = G::template base<LAST>(tl);
     double2* row_bl = row + G::template at<XL>(bl);
-    const double2* orow_bl = orow + G::template at<XL>(bl);
-    constexpr size_t GG = 4 * (size_t)M;  // complex values per Fourier GGSW: [r][c][m][lane]
+    const double2* orow_bl[K];  // the other polynomials' rows, ascending
+#pragma unroll
+    for (int q = 0; q < K; ++q) orow_bl[q] = xbuf + other_row<K>(P, q) * G::NP + G::template at<XL>(bl);
+    constexpr size_t GG = (size_t)(K + 1) * (K + 1) * M;  // complex values per Fourier GGSW: [r][c][m][lane]
     const int steps = (n + 1) / 2;
-    // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other row][m],
-    // and the lane's twiddles
-    double2 gv[3][2][LAT ? E : 1];
-    FTwr<M, LAT ? E : 2> twr;
-    if constexpr (LAT) ftw_load_phase<M, E, 0>(twr, tw, tl);
+    // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other rows][m],
+    // and (k = 1) the lane's twiddles
+    double2 gv[3][K + 1][LAT ? E : 1];
+    FTwr<M, TWR ? E : 2> twr;
+    if constexpr (TWR) ftw_load_phase<M, E, 0>(twr, tw, tl);
 #ifdef FR_BR_TIMING
     uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
@@ -476,11 +486,14 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
             for (int m = 0; m < E; ++m) {
 #ifdef FR_FFT_NOBSK  // timing experiment only (wrong results): no GGSW traffic
-                gv[gg][0][m] = make_double2(t + gg, m);
-                gv[gg][1][m] = make_double2(m, t - gg);
+#pragma unroll
+                for (int r = 0; r <= K; ++r) gv[gg][r][m] = make_double2(t + gg + r, m);
 #else
-                gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(3 * P) * M + (size_t)m * T)[tl];
-                gv[gg][1][m] = (bw + (size_t)gg * GG + (size_t)(2 - P) * M + (size_t)m * T)[tl];
+                gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(P * (K + 1) + P) * M + (size_t)m * T)[tl];
+#pragma unroll
+                for (int q = 0; q < K; ++q)
+                    gv[gg][1 + q][m] =
+                        (bw + (size_t)gg * GG + (size_t)(other_row<K>(P, q) * (K + 1) + P) * M + (size_t)m * T)[tl];
 #endif
             }
         };
@@ -517,9 +530,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int m = 0; m < E; ++m)
             x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
         FBR_STAMP(1);
-        // 2. forward FFT
-        if constexpr (LAT) {
-            fforward_from_r<M, E, 0>(x, row, twr, tl, [&](auto ph) {
+        // 2. forward FFT (latency shape: GGSW groups 1 and 2 issued at phase boundaries)
+        fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
+            if constexpr (LAT) {
                 constexpr int p = decltype(ph)::value;
                 if constexpr (p == FR_LAT_LOAD1) {
                     __builtin_amdgcn_sched_barrier(0);
@@ -531,10 +544,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                     load_ggsw(2);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-            });
-        } else {
-            fforward_from<M, E, 0, false>(x, row, tw, tl);
-        }
+            }
+        });
         FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #pragma unroll
@@ -547,27 +558,30 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #else
         constexpr bool PRE0 = !LAT;  // slot 0 lands during the MAC barrier and row exchange
 #endif
-        double2 Bc[3][2];
-        if constexpr (PRE0) load_slot<M, T>(Bc, bw, P, 0, tl);
+        double2 Bc[3][K + 1];
+        if constexpr (PRE0) load_slot<M, T, K>(Bc, bw, P, 0, tl);
         __syncthreads();
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
-        // Slot m of this lane has L = Lb + 1024 s_m: Lb = L mod 1024 is shared by the
+        // Slot m of this lane has L = Lb + M s_m: Lb = L mod M is shared by the
         // slots of equal m >> 2 (E/4 bases per lane) and s_m = brv2(m & 3) (fft.h: L(j) =
-        // 1 + 4 brv(j)).  psi^(1024 s e) = i^(s e) is an exact quarter turn (the table
+        // 1 + 4 brv(j)).  psi^(M s e) = i^(s e) is an exact quarter turn (the table
         // itself is quadrant-reduced), so one lookup per (e, base) serves every slot.
         // latency shape: computed at the top of the step (the lookups' LDS latency hides
         // behind the digits and the forward FFT); throughput shapes: here (VGPR budget)
         if constexpr (!LAT) psi_factors();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            double2 Bn[3][2];
+            double2 Bn[3][K + 1];
             if constexpr (AHEAD) {
-                if (m + 1 < E) load_slot<M, T>(Bn, bw, P, m + 1, tl);
+                if (m + 1 < E) load_slot<M, T, K>(Bn, bw, P, m + 1, tl);
                 __builtin_amdgcn_sched_barrier(0);
             } else if constexpr (!LAT) {
-                if (!PRE0 || m > 0) load_slot<M, T>(Bc, bw, P, m, tl);
+                if (!PRE0 || m > 0) load_slot<M, T, K>(Bc, bw, P, m, tl);
             }
-            const double2 own = x[m], oth = orow_bl[G::template at<XL>(G::template moff<LAST>(m))];
+            const double2 own = x[m];
+            double2 oth[K];
+#pragma unroll
+            for (int q = 0; q < K; ++q) oth[q] = orow_bl[q][G::template at<XL>(G::template moff<LAST>(m))];
             const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
             double cr[3], ci[3];
 #pragma unroll
@@ -577,32 +591,35 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             double zr, zi;
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
-                // y_g = D_P B_g[P][P] + D_(1-P) B_g[1-P][P]  (own row first)
-                const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
-                const double2 Bx = LAT ? gv[gg][1][LAT ? m : 0] : Bc[gg][1];
+                // y_g = D_P B_g[P][P] + sum_(r != P, ascending) D_r B_g[r][P]  (own row first)
                 double yr, yi;
-                fft::cmul(own.x, own.y, Bo.x, Bo.y, yr, yi);
-                fft::cmac(oth.x, oth.y, Bx.x, Bx.y, yr, yi);
+                {
+                    const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
+                    fft::cmul(own.x, own.y, Bo.x, Bo.y, yr, yi);
+                }
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const double2 Bx = LAT ? gv[gg][1 + q][LAT ? m : 0] : Bc[gg][1 + q];
+                    fft::cmac(oth[q].x, oth[q].y, Bx.x, Bx.y, yr, yi);
+                }
                 if (gg == 0) fft::cmul(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
                 else fft::cmac(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
             }
             x[m] = make_double2(zr, zi);
             if constexpr (!LAT) {
-                // keep the loads one slot ahead / in their slot, not all 6E hoisted (24E VGPRs)
+                // keep the loads one slot ahead / in their slot, not all hoisted
                 __builtin_amdgcn_sched_barrier(0);
             }
             if constexpr (AHEAD) {
 #pragma unroll
-                for (int gg = 0; gg < 3; ++gg) {
-                    Bc[gg][0] = Bn[gg][0];
-                    Bc[gg][1] = Bn[gg][1];
-                }
+                for (int gg = 0; gg < 3; ++gg)
+#pragma unroll
+                    for (int r = 0; r <= K; ++r) Bc[gg][r] = Bn[gg][r];
             }
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
-        if constexpr (LAT) finverse_from_r<M, E, LAST>(x, irow, twr, tl);
-        else finverse_from<M, E, LAST, false>(x, irow, tw, tl);
+        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, tl);
         FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -629,7 +646,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         accs[P * N + j + M] = ahi[m];
     }
     __syncthreads();
-    constexpr int K = 1, big = K * N;
+    constexpr int big = K * N;
     if (kind != JOB_MULTI) {
         uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
         const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
@@ -668,25 +685,38 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 }
 
 // ================================================================== host side
-static bool fft_supported(int N, int E) { return N == 2048 && (E == 4 || E == 8); }
+// compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
+// BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
+static bool fft_supported(int K, int N, int E) { return ((K == 1 && N == 2048) || (K == 2 && N == 1024)) && (E == 4 || E == 8); }
 
-template <int N, int E, bool LAT>
+template <int N, int K, int E, bool LAT>
 static void fft_attr() {
-    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, E, LAT>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)fbr_smem_bytes<N, E, LAT>()));
+    static_assert(fbr_smem_bytes<N, K, E, LAT>() <= (LAT ? 160 * 1024 : 160 * 1024 / fbr_tp_groups<K, E>()),
+                  "LDS per workgroup of the shape");
+    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, K, E, LAT>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbr_smem_bytes<N, K, E, LAT>()));
+}
+
+// run body(N, K) with the compile-time ring dimensions of the parameters
+template <class F>
+static void fft_dispatch(const Params& p, F&& body) {
+    if (p.k == 1 && p.N == 2048) body(std::integral_constant<int, 2048>{}, std::integral_constant<int, 1>{});
+    else if (p.k == 2 && p.N == 1024) body(std::integral_constant<int, 1024>{}, std::integral_constant<int, 2>{});
+    else throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N) in {(1, 2048), (2, 1024)}");
 }
 
 void Device::init_fft() {
+    if (p_.k == 2) fft_e_ = 8;  // one wave per polynomial: every transform exchange wave-local
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
-    if (p_.k != 1 || !fft_supported(p_.N, fft_e_))
-        throw Error(FR_ERR_INVALID, "device: FFT ring needs k = 1, N = 2048, E in {4, 8}");
-    static_assert(fbr_smem_bytes<2048, 4, true>() <= 160 * 1024, "latency shape: LDS");
-    static_assert(fbr_smem_bytes<2048, 4, false>() <= 80 * 1024 && fbr_smem_bytes<2048, 8, false>() <= 80 * 1024,
-                  "throughput shapes: two workgroups per CU");
-    fft_attr<2048, 4, true>();
-    fft_attr<2048, 4, false>();
-    fft_attr<2048, 8, false>();
+    if (!fft_supported(p_.k, p_.N, fft_e_))
+        throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N) in {(1, 2048), (2, 1024)}, E in {4, 8}");
+    fft_dispatch(p_, [&](auto nc, auto kc) {
+        constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
+        fft_attr<N, K, 4, true>();
+        fft_attr<N, K, 4, false>();
+        fft_attr<N, K, 8, false>();
+    });
     fft::Tables T(p_.N);
     FFT_CHECK(hipMalloc(&d_ftw_, 16 * (size_t)T.M));
     std::vector<fft::c64> psi(2 * (size_t)p_.N);
@@ -728,19 +758,22 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
 
 void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream) {
     const hipStream_t s = (hipStream_t)stream;
-    auto go = [&](auto ec, auto lat) {
-        constexpr int E = decltype(ec)::value;
-        constexpr bool LAT = decltype(lat)::value;
-        k_blind_rotate_fft<2048, E, LAT><<<(unsigned)n, fbr_threads<2048, E>(), fbr_smem_bytes<2048, E, LAT>(), s>>>(
-            d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_), (const double2*)d_ftw_,
-            (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
-    };
-    using I4 = std::integral_constant<int, 4>;
-    using I8 = std::integral_constant<int, 8>;
-    // small launches (at most one bootstrap per CU): the latency shape
-    if (n <= fft_small_) go(I4{}, std::true_type{});
-    else if (fft_e_ == 4) go(I4{}, std::false_type{});
-    else go(I8{}, std::false_type{});
+    fft_dispatch(p_, [&](auto nc, auto kc) {
+        constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
+        auto go = [&](auto ec, auto lat) {
+            constexpr int E = decltype(ec)::value;
+            constexpr bool LAT = decltype(lat)::value;
+            k_blind_rotate_fft<N, K, E, LAT><<<(unsigned)n, fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT>(), s>>>(
+                d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_),
+                (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
+        };
+        using I4 = std::integral_constant<int, 4>;
+        using I8 = std::integral_constant<int, 8>;
+        // small launches (at most one bootstrap per CU): the latency shape
+        if (n <= fft_small_) go(I4{}, std::true_type{});
+        else if (fft_e_ == 4) go(I4{}, std::false_type{});
+        else go(I8{}, std::false_type{});
+    });
     FFT_CHECK(hipGetLastError());
 }
 

@@ -248,8 +248,8 @@ void Device::encrypt_to_slots(const ClientKey& ck, const uint8_t* msgs, size_t c
 }
 
 void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
-    if (p_.ring != FR_RING_FFT || p_.N != 2048 || p_.k != 1)
-        throw Error(FR_ERR_INVALID, "device keygen: FFT ring (k = 1, N = 2048) only");
+    if (p_.ring != FR_RING_FFT || !((p_.N == 2048 && p_.k == 1) || (p_.N == 1024 && p_.k == 2)))
+        throw Error(FR_ERR_INVALID, "device keygen: FFT ring, (k, N) in {(1, 2048), (2, 1024)}");
     const int N = p_.N, M = N / 2, kp1 = p_.k + 1, n = p_.n, L = p_.ks_level;
     const size_t rows = (size_t)p_.big() * L, nw = p_.bsk_ggsw();
     const size_t bsk_polys = nw * kp1 * kp1;
@@ -297,7 +297,8 @@ void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
         d_tbsk_ = nullptr;
         KG_CHECK(hipMalloc(&d_tbsk_, 8 * p_.bsk_len()));
         const uint64_t gadget = 1ULL << (64 - p_.pbs_base_log);
-        k_gen_bsk<2048><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
+        if (N == 2048) k_gen_bsk<2048><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
+        else k_gen_bsk<1024><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
         KG_CHECK(hipGetLastError());
 
         // Fourier BSK in both lane layouts
@@ -308,8 +309,12 @@ void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
         }
         const int LOG = __builtin_ctz(M);
         const int L8 = geo_lo(LOG, 3, (LOG + 2) / 3 - 1), L4 = geo_lo(LOG, 2, (LOG + 1) / 2 - 1);
-        k_bsk_fourier<2048><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
-                                                                (double2*)d_fbsk_, (double2*)d_fbsk4_);
+        if (N == 2048)
+            k_bsk_fourier<2048><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
+                                                                    (double2*)d_fbsk_, (double2*)d_fbsk4_);
+        else
+            k_bsk_fourier<1024><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
+                                                                    (double2*)d_fbsk_, (double2*)d_fbsk4_);
         KG_CHECK(hipGetLastError());
         KG_CHECK(hipStreamSynchronize(s));
     } catch (...) {

@@ -196,8 +196,8 @@ def default_params(k: Optional[int] = None, N: Optional[int] = None, ring: Optio
         p.N = N
     if ring is not None:
         p.ring = ring
-    elif (p.k, p.N) != (1, 2048):
-        p.ring = RING_RNS  # the FFT ring is built for the reference's k = 1, N = 2048
+    elif (p.k, p.N) not in ((1, 2048), (2, 1024)):
+        p.ring = RING_RNS  # the FFT ring is built for k = 1, N = 2048 and k = 2, N = 1024
     return p
 
 

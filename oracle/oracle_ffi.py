@@ -140,12 +140,12 @@ RING_RNS, RING_FFT = 0, 1  # fheregex.h FR_RING_*
 def params_from_key(key: dict, k: int | None = None, N: int | None = None, ring: int | None = None) -> Params:
     """Reference params (k=1, N=2048) or the k=2, N=1024 reinterpretation of the
     same 2048-bit flattened GLWE key; ring: RING_FFT (2^64
-    torus, f64 FFT as tfhe-rs; the product's default at k=1, N=2048) or
-    RING_RNS (Z_Q, NTT; the only ring for k > 1)."""
+    torus, f64 FFT as tfhe-rs; the product's default at both points) or
+    RING_RNS (Z_Q, NTT)."""
     k = int(key["k"]) if k is None else k
     N = int(key["N"]) if N is None else N
     if ring is None:
-        ring = RING_FFT if (k, N) == (1, 2048) else RING_RNS
+        ring = RING_FFT if (k, N) in ((1, 2048), (2, 1024)) else RING_RNS
     assert k * N == len(key["s_big"])
     return Params(k, N, int(key["n"]), int(key["ks_base_log"]), int(key["ks_level"]),
                   int(key["pbs_base_log"]), int(key["pbs_level"]), ring, float(key["lwe_sigma"]),

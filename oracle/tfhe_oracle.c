@@ -421,12 +421,13 @@ void or_keygen_ksk(const or_params* P, const uint64_t* s_big, const uint64_t* s_
 }
 
 /* Bootstrapping-key unrolling (pairs of LWE coefficients per blind-rotation
- * step, k = 1): GGSW number w = 3t + g encrypts, for i = 2t, j = 2t+1,
+ * step; k = 1 on both rings, every k on the torus ring -- the product's
+ * Params::bsk_unroll): GGSW number w = 3t + g encrypts, for i = 2t, j = 2t+1,
  *   g = 0: s_i s_j,  g = 1: s_i (1 - s_j),  g = 2: (1 - s_i) s_j
  * (s_j = 0 past the end), so that X^(a_i s_i + a_j s_j) - 1 =
- * sum_g m_g (X^(e_g) - 1) with e = (a_i + a_j, a_i, a_j).  k > 1: one GGSW
- * of s_i per coefficient (no unrolling). */
-static int bsk_unroll(const or_params* P) { return P->k == 1 ? 2 : 1; }
+ * sum_g m_g (X^(e_g) - 1) with e = (a_i + a_j, a_i, a_j).  RNS ring, k > 1:
+ * one GGSW of s_i per coefficient (no unrolling). */
+static int bsk_unroll(const or_params* P) { return (P->k == 1 || P->ring == 1) ? 2 : 1; }
 static size_t bsk_ggsw(const or_params* P) {
     return bsk_unroll(P) == 2 ? 3 * (size_t)((P->n + 1) / 2) : (size_t)P->n;
 }

@@ -6,7 +6,9 @@ server key identical between the product's keygen and the oracle's, the
 oracle's blind rotation decrypting to the LUT values.  GPU: the device
 blind rotation (direct, multi-value, sign) and gate programs bit-exact
 against the oracle's restatement of the same operation sequence, and whole
-matches decrypting to the reference result."""
+matches decrypting to the reference result.  Both compiled points run: the
+reference's k = 1, N = 2048 and BASELINE's "N = 1024" set (k = 2, N = 1024,
+the same flattened 2048-bit key; ciphertext.rs:43-44 names the former)."""
 import ctypes as C
 import os
 
@@ -21,9 +23,18 @@ from conftest import GOLDEN
 SEED = 42
 
 
+POINTS = [(1, 2048), (2, 1024)]
+
+
+@pytest.fixture(scope="module", params=POINTS, ids=["k1n2048", "k2n1024"])
+def point(request):
+    return request.param
+
+
 @pytest.fixture(scope="module")
-def oracle_fft(fixture_key):
-    return of.Oracle(fixture_key, seed=SEED, ring=of.RING_FFT)
+def oracle_fft(fixture_key, point):
+    k, N = point
+    return of.Oracle(fixture_key, seed=SEED, k=k, N=N, ring=of.RING_FFT)
 
 
 def fft_mul(a, b):
@@ -63,20 +74,22 @@ def test_fft_product_exact_for_small_operands(N, abits, bbits):
     assert (fft_mul(a, b) == schoolbook(a, b)).all()
 
 
-def test_fft_tables_closed_forms():
+@pytest.mark.parametrize("N", [1024, 2048])
+def test_fft_tables_closed_forms(N):
     """The kernel computes leaf exponents in closed form, L(j) = 1 + 4 brv(j) (the
     slot of X^e's factor psi^(e L)); the twiddles are psi^((M >> (s+1)) (4 brv_s(b) + 1))
-    from the quadrant table, psi^(k + 1024 q) = i^q psi^k exactly."""
-    N, M = 2048, 1024
+    from the quadrant table, psi^(k + M q) = i^q psi^k exactly."""
+    M = N // 2
+    LOG = M.bit_length() - 1
     tw = np.zeros(2 * M)
     qt = np.zeros(N)
     leaf = np.zeros(M, dtype=np.uint16)
     of.lib().or_fft_tables(N, tw.ctypes.data_as(C.POINTER(C.c_double)), qt.ctypes.data_as(C.POINTER(C.c_double)),
                            leaf.ctypes.data_as(C.POINTER(C.c_uint16)))
     brv = lambda x, b: int(format(x, "0%db" % b)[::-1], 2) if b else 0
-    assert all(int(leaf[j]) == 1 + 4 * brv(j, 10) for j in range(M))
+    assert all(int(leaf[j]) == 1 + 4 * brv(j, LOG) for j in range(M))
     twc, qtc = tw.view(np.complex128), qt.view(np.complex128)
-    for s in range(10):
+    for s in range(LOG):
         for b in range(1 << s):
             q, r = divmod(((M >> (s + 1)) * (4 * brv(b, s) + 1)) % (2 * N), N // 2)
             z = qtc[r]
@@ -116,8 +129,8 @@ def test_torus_of_exact():
         assert L.or_torus_of(v) == e, (v, e)
 
 
-def test_torus_server_key_matches_oracle(key_blob, oracle_fft):
-    ctx = F.Context(device=-1, params=F.default_params(ring=F.RING_FFT))
+def test_torus_server_key_matches_oracle(key_blob, oracle_fft, point):
+    ctx = F.Context(device=-1, params=F.default_params(k=point[0], N=point[1], ring=F.RING_FFT))
     ctx.load_client_key(key_blob)
     ctx.gen_server_key(SEED)
     ksk, bsk = ctx.export_server_key()
@@ -127,28 +140,31 @@ def test_torus_server_key_matches_oracle(key_blob, oracle_fft):
 
 def test_torus_ggsw_rows_encrypt_gadget_times_key_bit(oracle_fft, fixture_key):
     """Row r of GGSW w decrypts (component phase) to m_w * 2^41 on component r's
-    coefficient 0 plus small noise."""
+    coefficient 0 plus small noise (k mask polynomials, body last)."""
     O = oracle_fft
-    N = O.P.N
-    s = O.s_big.astype(np.int64)
+    N, k = O.P.N, O.P.k
+    kp1 = k + 1
+    s = O.s_big.astype(np.int64).reshape(k, N)
     ss = O.s_small
     for w in (0, 1, 2, 99):
         t, g = divmod(w, 3)
         si, sj = int(ss[2 * t]), int(ss[2 * t + 1])
         m = [si & sj, si & (1 - sj), (1 - si) & sj][g]
-        for r in range(2):
-            row = O.bsk[(w * 2 + r) * 2 * N:(w * 2 + r + 1) * 2 * N].reshape(2, N)
-            A, B = row[0].astype(np.uint64), row[1].astype(np.uint64)
-            # phase = B - A*S (negacyclic), mod 2^64, computed exactly with Python ints on a few coefficients
+        for r in range(kp1):
+            row = O.bsk[(w * kp1 + r) * kp1 * N:(w * kp1 + r + 1) * kp1 * N].reshape(kp1, N)
+            B = row[k].astype(np.uint64)
+            # phase = B - sum_j A_j*S_j (negacyclic), mod 2^64, computed exactly with Python ints on a few coefficients
             for c in (0, 1, N - 1):
                 acc = int(B[c])
-                for u in np.nonzero(s)[0]:
-                    src = c - u
-                    acc -= int(A[src]) if src >= 0 else -int(A[src + N])
+                for j in range(k):
+                    A = row[j].astype(np.uint64)
+                    for u in np.nonzero(s[j])[0]:
+                        src = c - u
+                        acc -= int(A[src]) if src >= 0 else -int(A[src + N])
                 acc %= 1 << 64
-                # gadget on component r: +2^41 on the body (r = 1) is +2^41 in the
-                # phase; on the mask (r = 0) it is -2^41 * S_c
-                expect = (m << 41) if (c == 0 and r == 1) else (-(m << 41) * int(s[c]) if r == 0 else 0)
+                # gadget on component r: +2^41 on the body (r = k) is +2^41 in the
+                # phase; on mask j = r it is -2^41 * S_r[c] (X^0 times the key polynomial)
+                expect = (m << 41) if (c == 0 and r == k) else (-(m << 41) * int(s[r][c]) if r < k else 0)
                 err = (acc - expect) % (1 << 64)
                 err = err - (1 << 64) if err >= 1 << 63 else err
                 assert abs(err) < 1 << 20, (w, r, c)
@@ -168,8 +184,8 @@ def test_oracle_fft_blind_rotation_decrypts(oracle_fft, msgs):
 
 # ------------------------------------------------------------------- GPU
 @pytest.fixture(scope="module")
-def fctx(key_blob):
-    ctx = F.Context(device=0, params=F.default_params(ring=F.RING_FFT))
+def fctx(key_blob, point):
+    ctx = F.Context(device=0, params=F.default_params(k=point[0], N=point[1], ring=F.RING_FFT))
     ctx.load_client_key(key_blob)
     ctx.gen_server_key(SEED)
     return ctx

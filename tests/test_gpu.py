@@ -22,10 +22,16 @@ def load(name):
         return json.load(f)
 
 
-@pytest.fixture(scope="module", params=[F.RING_FFT, F.RING_RNS], ids=["fft", "rns"])
+# (ring, k, N): the reference's parameters on both blind-rotation rings, and
+# BASELINE's "N = 1024" set (k = 2, N = 1024) on the FFT ring
+POINTS = [(F.RING_FFT, 1, 2048), (F.RING_RNS, 1, 2048), (F.RING_FFT, 2, 1024)]
+
+
+@pytest.fixture(scope="module", params=POINTS, ids=["fft", "rns", "fft-k2n1024"])
 def gctx(request, key_blob):
-    """Every test below runs on both blind-rotation rings."""
-    ctx = F.Context(device=0, params=F.default_params(ring=request.param))
+    """Every test below runs at every point."""
+    ring, k, N = request.param
+    ctx = F.Context(device=0, params=F.default_params(k=k, N=N, ring=ring))
     ctx.load_client_key(key_blob)
     ctx.gen_server_key(SEED)
     return ctx
@@ -33,8 +39,9 @@ def gctx(request, key_blob):
 
 @pytest.fixture(scope="module")
 def oracle_k1(gctx, fixture_key):
-    """Oracle keys on the context's ring (server-key seed 42)."""
-    return of.Oracle(fixture_key, seed=SEED, ring=gctx.params.ring)
+    """Oracle keys at the context's point (server-key seed 42)."""
+    p = gctx.params
+    return of.Oracle(fixture_key, seed=SEED, k=p.k, N=p.N, ring=p.ring)
 
 
 def test_device_info(gctx):
@@ -371,13 +378,14 @@ def test_plan_cache_replays_bit_identical(gctx):
         gctx.release(h)
 
 
-def test_k2_n1024_params(key_blob, fixture_key):
-    """The N=1024 variant: the same 2048-bit key read as k=2 polynomials of 1024."""
-    params = F.default_params(k=2, N=1024)
+def test_k2_n1024_params_rns(key_blob, fixture_key):
+    """The N=1024 variant on the RNS ring (one GGSW per coefficient): the same
+    2048-bit key read as k=2 polynomials of 1024."""
+    params = F.default_params(k=2, N=1024, ring=F.RING_RNS)
     ctx = F.Context(0, params)
     ctx.load_client_key(key_blob)
     ctx.gen_server_key(SEED)
-    O = of.Oracle(fixture_key, seed=SEED, k=2, N=1024)
+    O = of.Oracle(fixture_key, seed=SEED, k=2, N=1024, ring=of.RING_RNS)
     ksk, bsk = ctx.export_server_key()
     assert (ksk == O.ksk).all() and (bsk == O.bsk).all()
     blocks = O.encrypt_blocks([6, 1], seed=5)

@@ -72,3 +72,23 @@ def test_device_key_runs_bit_exact(key_blob):
         outs.append(ctx.download_radix(out))
         assert ctx.decrypt_radix(outs[-1]) == 1
     assert np.array_equal(outs[0], outs[1])
+
+
+@pytest.mark.gpu
+def test_device_keygen_k2n1024_matches_host(key_blob):
+    """BASELINE's "N = 1024" point (k = 2, N = 1024, FFT ring): k_gen_bsk<1024>
+    and k_bsk_fourier<1024> against the host generator, then one match."""
+    params = F.default_params(k=2, N=1024, ring=F.RING_FFT)
+    keys = []
+    for where in (F.KEYGEN_DEVICE, F.KEYGEN_HOST):
+        ctx = F.Context(device=0 if where == F.KEYGEN_DEVICE else -1, params=params)
+        ctx.load_client_key(key_blob)
+        ctx.set_keygen(where)
+        ctx.gen_server_key(SEED)
+        keys.append(ctx.export_server_key())
+        if where == F.KEYGEN_DEVICE:
+            hs = ctx.upload_radix(ctx.encrypt_str("zabcz", seed=3))
+            out, _ = ctx.has_match(hs, "/abc/")
+            assert ctx.decrypt_radix(ctx.download_radix(out)) == 1
+    assert np.array_equal(keys[0][0], keys[1][0])
+    assert np.array_equal(keys[0][1], keys[1][1])
