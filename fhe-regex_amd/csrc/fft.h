@@ -51,14 +51,17 @@ FR_HD void cmac(double ar, double ai, double br, double bi, double& zr, double& 
     zr = FR_FMA(-ai, bi, FR_FMA(ar, br, zr));
     zi = FR_FMA(ai, br, FR_FMA(ar, bi, zi));
 }
-// forward butterfly: t = c * hi; (lo, hi) <- (lo + t, lo - t)
+// forward butterfly (lo, hi) <- (lo + c hi, lo - c hi) in six fused operations:
+//   lo' = (fma(c.re, hi.re, fma(-c.im, hi.im, lo.re)), fma(c.re, hi.im, fma(c.im, hi.re, lo.im)))
+//   hi' = 2 lo - lo' = (fma(2, lo.re, -lo'.re), fma(2, lo.im, -lo'.im))
+// (the absolute error of hi' is that of lo', one rounding of |lo| + |c hi|)
 FR_HD void fwd_bf(double& xr, double& xi, double& yr, double& yi, double cr, double ci) {
-    double tr, ti;
-    cmul(cr, ci, yr, yi, tr, ti);
-    yr = xr - tr;
-    yi = xi - ti;
-    xr = xr + tr;
-    xi = xi + ti;
+    const double ur = FR_FMA(cr, yr, FR_FMA(-ci, yi, xr));
+    const double ui = FR_FMA(cr, yi, FR_FMA(ci, yr, xi));
+    yr = FR_FMA(2.0, xr, -ur);
+    yi = FR_FMA(2.0, xi, -ui);
+    xr = ur;
+    xi = ui;
 }
 // inverse butterfly: d = u - v; (u, v) <- (u + v, conj(c) * d)
 //   conj(c) d: re = fma(c.re, d.re, c.im d.im), im = fma(c.re, d.im, -(c.im d.re))
@@ -103,15 +106,26 @@ FR_HD uint64_t torus_of(double v) {
     const double lo = FR_FMA(-hi, 0x1p32, ri);
     return ((uint64_t)(uint32_t)hm << 32) | (uint64_t)(uint32_t)lo;
 }
-// signed gadget digit of a torus value: base 2^B, one level (B = pbs_base_log),
-// closest multiple of 2^(64-B) (round half up), digit in [-2^(B-1), 2^(B-1))
+// The blind rotation's accumulator is f64: a torus value t (mod 2^64) is held as a
+// double in [-2^63, 2^63] congruent to t up to the rounding of the additions (below
+// 2^44 per step, far under the bootstrap noise).  Per step:
+//   digit  d = rint(a 2^-(64-B)) in [-2^(B-1), 2^(B-1)] (one level, base 2^B: the
+//          closest multiple of 2^(64-B), ties to even)
+//   update a = reduce(a + v), v the inverse transform's f64 output (|v| < 2^100),
+//          reduce(a) = fma(-rint(a 2^-64), 2^64, a), exact
+// and torus_of(a) gives the u64 torus value for sample extraction.
+#if defined(__HIPCC__)
+#define FR_RINT(x) __builtin_rint(x)
+#else
+#define FR_RINT(x) std::nearbyint(x)
+#endif
 template <int B>
-FR_HD int32_t pbs_digit(uint64_t a) {
-    // (a >> (64-B)) + bit (63-B), mod 2^B, recentred: on the high word, add half a
-    // digit unit and keep the top B bits as a signed field
-    static_assert(B >= 1 && B <= 31, "one-level digit inside the high word");
-    return (int32_t)((uint32_t)(a >> 32) + (1u << (31 - B))) >> (32 - B);
+FR_HD double acc_digit(double a) {
+    return FR_RINT(a * (1.0 / (double)(1ULL << (64 - B))));
 }
+FR_HD double acc_reduce(double a) { return FR_FMA(-FR_RINT(a * 0x1p-64), 0x1p64, a); }
+// exact f64 of a u64 torus value, as the signed representative in [-2^63, 2^63)
+FR_HD double acc_of_torus(uint64_t t) { return (double)(int64_t)t; }
 
 // ---------------------------------------------------------------- host side
 // psi^x (x mod 2N) = i^q (cos(pi r / N), sin(pi r / N)), x = q N/2 + r

@@ -435,9 +435,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         Lb[bb] = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 4 * bb)) >> (32 - G::LOG))) & (uint32_t)(M - 1);
     __syncthreads();
 
-    // accumulator (u64 torus), natural order: lane holds coefficients j and j + M
-    // for j = idx<0>(tl, m); mask polynomials 0, body (polynomial K) X^-bbar * V
-    uint64_t alo[E], ahi[E];
+    // accumulator (f64 torus, fft.h), natural order: lane holds coefficients j and
+    // j + M for j = idx<0>(tl, m); mask polynomials 0, body (polynomial K) X^-bbar * V
+    double alo[E], ahi[E];
     {
         const bool direct = kind == JOB_DIRECT;
 #pragma unroll
@@ -450,8 +450,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut);
                 v[h] = s < N ? tv : (uint64_t)0 - tv;
             }
-            alo[m] = P == K ? v[0] : 0;
-            ahi[m] = P == K ? v[1] : 0;
+            alo[m] = P == K ? fft::acc_of_torus(v[0]) : 0.0;
+            ahi[m] = P == K ? fft::acc_of_torus(v[1]) : 0.0;
         }
     }
 
@@ -527,8 +527,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
         double2 x[E];
 #pragma unroll
-        for (int m = 0; m < E; ++m)
-            x[m] = make_double2((double)fft::pbs_digit<23>(alo[m]), (double)fft::pbs_digit<23>(ahi[m]));
+        for (int m = 0; m < E; ++m) x[m] = make_double2(fft::acc_digit<23>(alo[m]), fft::acc_digit<23>(ahi[m]));
         FBR_STAMP(1);
         // 2. forward FFT (latency shape: GGSW groups 1 and 2 issued at phase boundaries)
         fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
@@ -618,13 +617,13 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             }
         }
         FBR_STAMP(3);
-        // 4. inverse FFT (times M; 1/M is in the key), back to the torus, accumulate
+        // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
         finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, tl);
         FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
-            alo[m] += fft::torus_of(x[m].x);
-            ahi[m] += fft::torus_of(x[m].y);
+            alo[m] = fft::acc_reduce(alo[m] + x[m].x);
+            ahi[m] = fft::acc_reduce(ahi[m] + x[m].y);
         }
         FBR_STAMP(5);
     }
@@ -642,8 +641,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
     for (int m = 0; m < E; ++m) {
         const int j = G::template idx<0>(tl, m);
-        accs[P * N + j] = alo[m];
-        accs[P * N + j + M] = ahi[m];
+        accs[P * N + j] = fft::torus_of(alo[m]);
+        accs[P * N + j + M] = fft::torus_of(ahi[m]);
     }
     __syncthreads();
     constexpr int big = K * N;

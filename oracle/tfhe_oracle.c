@@ -288,18 +288,19 @@ static fft_plan* fft_plan_make(int N) {
     return F;
 }
 static void fft_plan_free(fft_plan* F) { free(F->tw); free(F->qt); free(F->leaf); free(F); }
-/* forward: (lo, hi) -> (lo + c hi, lo - c hi), natural order -> slot order */
+/* forward: (lo, hi) -> (lo + c hi, lo - c hi), natural order -> slot order;
+ * lo + c hi as two nested fmas per component, lo - c hi as 2 lo - (lo + c hi) */
 static void fft_forward(const fft_plan* F, cplx* z) {
     for (int s = 0; s < F->LOG; s++) {
         int h = F->M >> (s + 1);
         for (int b = 0; b < (1 << s); b++) {
             cplx c = F->tw[(1 << s) + b];
             for (int j = b * 2 * h; j < b * 2 * h + h; j++) {
-                double tr, ti;
-                c_mul(c.re, c.im, z[j + h].re, z[j + h].im, &tr, &ti);
-                double xr = z[j].re, xi = z[j].im;
-                z[j + h].re = xr - tr; z[j + h].im = xi - ti;
-                z[j].re = xr + tr; z[j].im = xi + ti;
+                double xr = z[j].re, xi = z[j].im, yr = z[j + h].re, yi = z[j + h].im;
+                double ur = fma(c.re, yr, fma(-c.im, yi, xr));
+                double ui = fma(c.re, yi, fma(c.im, yr, xi));
+                z[j + h].re = fma(2.0, xr, -ur); z[j + h].im = fma(2.0, xi, -ui);
+                z[j].re = ur; z[j].im = ui;
             }
         }
     }
@@ -330,11 +331,11 @@ static inline uint64_t torus_of(double v) {
     double hu = hi < 0 ? hi + 0x1p32 : hi;
     return ((uint64_t)(uint32_t)hu << 32) + (uint64_t)(uint32_t)lo;
 }
-/* signed one-level gadget digit, base 2^B: closest multiple of 2^(64-B) */
-static inline int64_t torus_digit(uint64_t a, int B) {
-    uint64_t c = ((a >> (64 - B)) + ((a >> (63 - B)) & 1)) & ((1ULL << B) - 1);
-    return c >= (1ULL << (B - 1)) ? (int64_t)c - (1LL << B) : (int64_t)c;
-}
+/* f64 blind-rotation accumulator (fft.h): a torus value held as a double in
+ * [-2^63, 2^63]; digit rint(a 2^-(64-B)); update reduce(a + v) with
+ * reduce(a) = fma(-rint(a 2^-64), 2^64, a) (exact) */
+static inline double acc_digit(double a, int B) { return nearbyint(a * ldexp(1.0, B - 64)); }
+static inline double acc_reduce(double a) { return fma(-nearbyint(a * 0x1p-64), 0x1p64, a); }
 /* negacyclic product mod 2^64 through the FFT (test hook: b must be small,
  * |b| * |a| * N < 2^50, for an exact result) and exactly (schoolbook) */
 void or_fft_ring_mul(int N, const int64_t* a, const int64_t* b, int64_t* out) {
@@ -671,6 +672,7 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
     const fft_plan* F = K->FP;
     int k = P->k, N = P->N, n = P->n, M = N / 2, log2N2 = ilog2(2 * N);
     size_t kp1 = (size_t)k + 1, big = (size_t)k * N;
+    double* dacc = calloc(kp1 * N, sizeof(double)); /* f64 accumulator (fft.h) */
     uint64_t* acc = calloc(kp1 * N, 8);
     cplx* D = malloc(sizeof(cplx) * kp1 * M);
     cplx* Z = malloc(sizeof(cplx) * M);
@@ -686,7 +688,7 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
     uint32_t b = mod_switch(ks_lwe[n], log2N2);
     for (int j = 0; j < N; j++) {
         int s = (j + (int)b) & (2 * N - 1);
-        acc[(size_t)k * N + j] = s < N ? V[s] : (uint64_t)0 - V[s - N];
+        dacc[(size_t)k * N + j] = (double)(int64_t)(s < N ? V[s] : (uint64_t)0 - V[s - N]);
     }
     for (int i = 0; i < n; i += 2) {
         uint32_t ai = mod_switch(ks_lwe[i], log2N2);
@@ -695,8 +697,8 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
         for (size_t c = 0; c < kp1; c++) {
             cplx* Dc = D + c * M;
             for (int t = 0; t < M; t++) {
-                Dc[t].re = (double)torus_digit(acc[c * N + t], P->pbs_base_log);
-                Dc[t].im = (double)torus_digit(acc[c * N + t + M], P->pbs_base_log);
+                Dc[t].re = acc_digit(dacc[c * N + t], P->pbs_base_log);
+                Dc[t].im = acc_digit(dacc[c * N + t + M], P->pbs_base_log);
             }
             fft_forward(F, Dc);
         }
@@ -727,11 +729,12 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
             }
             fft_inverse(F, Z);
             for (int t = 0; t < M; t++) {
-                acc[c * N + t] += torus_of(Z[t].re);
-                acc[c * N + t + M] += torus_of(Z[t].im);
+                dacc[c * N + t] = acc_reduce(dacc[c * N + t] + Z[t].re);
+                dacc[c * N + t + M] = acc_reduce(dacc[c * N + t + M] + Z[t].im);
             }
         }
     }
+    for (size_t c = 0; c < kp1 * (size_t)N; c++) acc[c] = torus_of(dacc[c]);
     int32_t pos[17], d[17];
     for (int f = 0; f < (direct ? 1 : n_out); f++) {
         uint64_t* out = outs + (size_t)f * (big + 1);
@@ -753,7 +756,7 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
         }
         if (direct == 2) out[big] += 1ULL << 58;
     }
-    free(acc); free(D); free(Z); free(V);
+    free(acc); free(dacc); free(D); free(Z); free(V);
 }
 
 void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts, int n_out, int direct, uint64_t* outs) {
