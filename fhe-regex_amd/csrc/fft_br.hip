@@ -36,7 +36,9 @@ namespace fr {
     } while (0)
 
 template <int M, int E>
-using FGeo = NttGeo<M, E, 3>;
+using FGeo = NttGeo<M, E, 3, fft_layout_variant(ilog2c(M), ilog2c(E))>;
+template <int M, int E>
+constexpr int FV = fft_layout_variant(ilog2c(M), ilog2c(E));
 
 // FR_BR_TIMING (debug builds only): wave 0 of workgroup 0 accumulates
 // s_memtime deltas of the step segments and prints them at the end.
@@ -157,10 +159,8 @@ __device__ __forceinline__ void finv_phase_r(double2 (&x)[E], const FTwr<M, E>& 
 template <int M, int E, int PF, int PT>
 constexpr bool fwave_local() {
     using G = FGeo<M, E>;
-    for (int b = 6; (1 << b) < G::T; ++b) {
-        const int f = b < G::lo(PF) ? b : b + G::e, t = b < G::lo(PT) ? b : b + G::e;
-        if (f != t) return false;
-    }
+    for (int b = 6; (1 << b) < G::T; ++b)
+        if (G::lane_bit(PF, b) != G::lane_bit(PT, b)) return false;
     return true;
 }
 __device__ __forceinline__ void fwave_sync() {
@@ -182,8 +182,8 @@ constexpr int fperm_lane_bit(int j) {
     const int out = G::lo(PF) + j, in = G::lo(PT) + j;
     int kb = -1, kc = -1;
     for (int b = 0; b < 6; ++b) {
-        if (geo_lane_bit(G::LOG, G::e, PT, b) == out) kb = b;
-        if (geo_lane_bit(G::LOG, G::e, PF, b) == in) kc = b;
+        if (G::lane_bit(PT, b) == out) kb = b;
+        if (G::lane_bit(PF, b) == in) kc = b;
     }
     return kb == kc ? kb : -1;
 }
@@ -202,7 +202,7 @@ constexpr bool fperm_ok() {
     for (int b = 0; b < 8; ++b) {
         bool swapped = false;
         for (int j = 0; j < G::e; ++j) swapped |= fperm_lane_bit<M, E, PF, PT>(j) == b;
-        if (!swapped && geo_lane_bit(G::LOG, G::e, PF, b) != geo_lane_bit(G::LOG, G::e, PT, b)) return false;
+        if (!swapped && G::lane_bit(PF, b) != G::lane_bit(PT, b)) return false;
     }
     return true;
 #endif
@@ -267,11 +267,15 @@ template <int M, int E, int p>
 constexpr bool finv_pre() {
     return p == FGeo<M, E>::NPH - 1 || !FGeo<M, E>::wave_top(p);
 }
+// every LDS exchange conflict-free; register exchanges need no map, except that map XL
+// also serves the MAC's last-layout accesses
 template <int M, int E, int X = 0>
 constexpr bool fexchanges_conflict_free() {
     using G = FGeo<M, E>;
     if constexpr (X + 1 >= G::NPH) return true;
-    else return G::template b128_exchange_ok<X>() && fexchanges_conflict_free<M, E, X + 1>();
+    else
+        return ((fperm_ok<M, E, X, X + 1>() && X != G::XL) || G::template b128_exchange_ok<X>()) &&
+               fexchanges_conflict_free<M, E, X + 1>();
 }
 // NOPRE: the rows of the forward transform + MAC and of the inverse transform
 // are separate buffers (latency shape).  Then no write needs a barrier before
@@ -281,25 +285,29 @@ constexpr bool fexchanges_conflict_free() {
 // polynomials' MAC reads.
 // TWR: twiddles from the lane's registers (twr), else from the LDS table tw.
 // hook(integral_constant<p>) runs after phase p's butterflies (before its exchange).
-template <int M, int E, int p, bool NOPRE, bool TWR, class Hook>
+// CARRY: a pre-barrier owed by a register exchange (which writes no LDS) moves to the
+// next LDS exchange's write.
+template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false, class Hook>
 __device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, int tl, Hook&& hook) {
     if constexpr (TWR) ffwd_phase_r<M, E, p>(x, twr);
     else ffwd_phase<M, E, p>(x, tw, tl);
     hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
-        fexchange<M, E, p, p + 1, !NOPRE && ffwd_pre<M, E, p>()>(x, row, tl);
-        fforward_from<M, E, p + 1, NOPRE, TWR>(x, row, twr, tw, tl, hook);
+        constexpr bool pre = !NOPRE && (ffwd_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p + 1>();
+        fexchange<M, E, p, p + 1, reg ? false : pre>(x, row, tl);
+        fforward_from<M, E, p + 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl, hook);
     }
 }
-template <int M, int E, int p, bool NOPRE, bool TWR>
+template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false>
 __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, int tl) {
     if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
     else finv_phase<M, E, p>(x, tw, tl);
     if constexpr (p > 0) {
-        fexchange<M, E, p, p - 1, !NOPRE && finv_pre<M, E, p>()>(x, row, tl);
-        finverse_from<M, E, p - 1, NOPRE, TWR>(x, row, twr, tw, tl);
+        constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
+        fexchange<M, E, p, p - 1, reg ? false : pre>(x, row, tl);
+        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl);
     }
 }
 
@@ -716,6 +724,7 @@ void Device::init_fft() {
         fft_attr<N, K, 4, false>();
         fft_attr<N, K, 8, false>();
     });
+
     fft::Tables T(p_.N);
     FFT_CHECK(hipMalloc(&d_ftw_, 16 * (size_t)T.M));
     std::vector<fft::c64> psi(2 * (size_t)p_.N);
@@ -740,13 +749,13 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
         const int T = M / E;
         int e = 0;
         while ((1 << e) < E) ++e;
-        const int L = geo_lo(tabs.LOG, e, (tabs.LOG + e - 1) / e - 1);
+        const int LAST = (tabs.LOG + e - 1) / e - 1, L = geo_lo(tabs.LOG, e, LAST);
+        const int V = fft_layout_variant(tabs.LOG, e);
+        std::vector<int> slot((size_t)T * E);
+        for (int tl = 0; tl < T; ++tl)
+            for (int m = 0; m < E; ++m) slot[(size_t)m * T + tl] = geo_base(tabs.LOG, e, LAST, tl, V) + (m << L);
         for (size_t pq = 0; pq < polys; ++pq)
-            for (int tl = 0; tl < T; ++tl)
-                for (int m = 0; m < E; ++m) {
-                    const int slot = (((tl >> L) << (L + e)) | (tl & ((1 << L) - 1))) + (m << L);
-                    lanes[pq * M + (size_t)m * T + tl] = four[pq * M + slot];
-                }
+            for (size_t q = 0; q < (size_t)M; ++q) lanes[pq * M + q] = four[pq * M + slot[q]];
         double*& dst = E == 8 ? d_fbsk_ : d_fbsk4_;
         (void)hipFree(dst);
         dst = nullptr;

@@ -35,10 +35,36 @@ struct LdsMap {
     int span;
 };
 constexpr int geo_lo(int LOG, int e, int p) { return LOG - (p + 1) * e > 0 ? LOG - (p + 1) * e : 0; }
-constexpr int geo_lane_bit(int LOG, int e, int p, int b) { return b < geo_lo(LOG, e, p) ? b : b + e; }
-constexpr unsigned geo_group(int LOG, int e, int p, int GB) {
+// Layout p sends lane bit b to index bit geo_lane_bit(.., p, b); phase p's E elements
+// are the index bits [lo(p), lo(p) + e).  Layout family V:
+//  V = 0: lane bits keep their order around the element bits (b < lo(p): b, else b + e).
+//  V = 1 (M = 1024, E = 4, 256 lanes: the f64 FFT of k = 1): layouts 3 and 4 put lane
+//    bits 0..3 on index bits 4, 5, 7, 6 (bit 6 last: it is lane bit 4 of layout 2, whose
+//    b128 reads want it off the write groups' lane bits 0..2 of layout 3) and lane bits
+//    4, 5 on the other phase's element bits
+//    (layout 3: 0, 1; layout 4: 2, 3), so that the exchange 3 <-> 4, like 1 <-> 2,
+//    swaps element bits with lane bits 4 and 5 (v_permlane16/32_swap, no LDS); the
+//    other layouts are V = 0's.
+constexpr int geo_lane_bit(int LOG, int e, int p, int b, int V = 0) {
+    if (V == 1 && p >= 3) {
+        if (b < 4) return b < 2 ? 4 + b : 9 - b;
+        if (b < 6) return (p == 3 ? 0 : 2) + (b - 4);
+        return b + 2;
+    }
+    return b < geo_lo(LOG, e, p) ? b : b + e;
+}
+// index of element 0 of lane tl in layout p (host and compile-time use)
+constexpr int geo_base(int LOG, int e, int p, int tl, int V = 0) {
+    int idx = 0;
+    for (int b = 0; (tl >> b) != 0; ++b)
+        if ((tl >> b) & 1) idx |= 1 << geo_lane_bit(LOG, e, p, b, V);
+    return idx;
+}
+// the layout family of the f64 FFT kernels (fft_br.hip, keygen.hip, the key upload)
+constexpr int fft_layout_variant(int LOG, int e) { return LOG == 10 && e == 2 ? 1 : 0; }
+constexpr unsigned geo_group(int LOG, int e, int p, int GB, int V = 0) {
     unsigned g = 0;
-    for (int b = 0; b < GB; ++b) g |= 1u << geo_lane_bit(LOG, e, p, b);
+    for (int b = 0; b < GB; ++b) g |= 1u << geo_lane_bit(LOG, e, p, b, V);
     return g;
 }
 constexpr LdsMap make_lds_map(int LOG, int e, int H, int x, int nph, int GB) {
@@ -98,19 +124,28 @@ struct B128Req {
     int ge4[4] = {};     // index bits that need valuation >= 4
     int nge4 = 0;
 };
-constexpr B128Req b128_requirements(int LOG, int e, int x, int nph) {
+// map x serves the exchange x <-> x+1; with V = 1 the exchange (nph-2) <-> (nph-1) is a
+// register exchange and map nph-2 serves only the MAC's last-layout accesses
+constexpr bool b128_mac_only(int x, int nph, int V) { return V == 1 && x == nph - 2; }
+// V = 1, exchange 2 <-> 3: index bit 6 is lane bit 4 of layout 2 and one of lane bits 0..3
+// of layout 3 (index bit 0 the other way round), so the reads of one of the two layouts
+// cannot be conflict-free; layout 3's reads (the forward exchange) take 2-way conflicts
+constexpr int b128_relaxed_read(int x, int V) { return V == 1 && x == 2 ? 3 : -1; }
+constexpr B128Req b128_requirements(int LOG, int e, int x, int nph, int V = 0) {
     B128Req q{};
     const int xt = x + 1 < nph ? x + 1 : x;
-    const int dirs[2][2] = {{x, xt}, {xt, x}};  // (written layout, read layout)
+    const int xf = b128_mac_only(x, nph, V) ? xt : x;
+    const int dirs[2][2] = {{xf, xt}, {xt, xf}};  // (written layout, read layout)
     for (int d = 0; d < 2; ++d) {
         const int W = dirs[d][0], R = dirs[d][1];
         q.size[q.nset] = 3;
-        for (int b = 0; b < 3; ++b) q.set[q.nset][b] = geo_lane_bit(LOG, e, W, b);
+        for (int b = 0; b < 3; ++b) q.set[q.nset][b] = geo_lane_bit(LOG, e, W, b, V);
         ++q.nset;
+        if (R == b128_relaxed_read(x, V)) continue;
         q.size[q.nset] = 4;
-        for (int b = 0; b < 4; ++b) q.set[q.nset][b] = geo_lane_bit(LOG, e, R, b);
+        for (int b = 0; b < 4; ++b) q.set[q.nset][b] = geo_lane_bit(LOG, e, R, b, V);
         ++q.nset;
-        q.ge4[q.nge4++] = geo_lane_bit(LOG, e, R, 4);
+        q.ge4[q.nge4++] = geo_lane_bit(LOG, e, R, 4, V);
     }
     return q;
 }
@@ -147,9 +182,9 @@ constexpr int val2(int w) {
     }
     return v;
 }
-constexpr LdsMap make_b128_map(int LOG, int e, int H, int x, int nph) {
+constexpr LdsMap make_b128_map(int LOG, int e, int H, int x, int nph, int V = 0) {
     LdsMap m{};
-    const B128Req q = b128_requirements(LOG, e, x, nph);
+    const B128Req q = b128_requirements(LOG, e, x, nph, V);
     int val[16] = {-1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1, -1};
     if (!b128_solve(q, val, 0, H)) {
         m.span = -1;  // caught by the conflict check
@@ -197,11 +232,11 @@ struct LdsMaps {
     LdsMap m[8];
     int ch;
 };
-constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph, int GB) {
+constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph, int GB, int V = 0) {
     LdsMaps r{};
     r.ch = 1 << GB;
     for (int x = 0; x < (nph > 1 ? nph - 1 : 1); ++x) {
-        r.m[x] = GB == 3 ? make_b128_map(LOG, e, H, x, nph) : make_lds_map(LOG, e, H, x, nph, GB);
+        r.m[x] = GB == 3 ? make_b128_map(LOG, e, H, x, nph, V) : make_lds_map(LOG, e, H, x, nph, GB);
         if (r.m[x].span > r.ch) r.ch = r.m[x].span;
     }
     return r;
@@ -212,7 +247,7 @@ constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph, int GB) {
 // log2 E stages; phase p's lane owns the E elements that differ in index bits
 // [lo(p), lo(p)+e), and two consecutive phases are joined by one LDS
 // exchange.  Forward stage s pairs bit LOG-1-s with zeta[(1<<s) + (j >> (LOG-s))].
-template <int N, int E, int GB = 5>
+template <int N, int E, int GB = 5, int V = 0>
 struct NttGeo {
     static constexpr int LOG = ilog2c(N);
     static constexpr int e = ilog2c(E);
@@ -228,12 +263,15 @@ struct NttGeo {
     // last-phase (bit-reversed slot) accesses of the MAC.
     static constexpr int WB = ilog2c(T / 64);  // wave bits of a row
     static constexpr int H = LOG - WB;
-    static constexpr LdsMaps MAPS = make_lds_maps(LOG, e, H, NPH, GB);
+    static constexpr LdsMaps MAPS = make_lds_maps(LOG, e, H, NPH, GB, V);
+    static_assert(V == 0 || (LOG == 10 && e == 2 && T == 256), "layout family V = 1: M = 1024, E = 4");
+    static constexpr int lane_bit(int p, int b) { return geo_lane_bit(LOG, e, p, b, V); }
     static constexpr int CH = MAPS.ch;
     static constexpr int NP = CH << WB;  // LDS row (elements)
     static constexpr int XL = NPH >= 2 ? NPH - 2 : 0;
     // the wave bits of layout p are its top index bits [H, LOG)
     static constexpr bool wave_top(int p) { return WB == 0 || lo(p) <= 6; }
+    static_assert(V == 0 || (lane_bit(3, 6) == 8 && lane_bit(4, 7) == 9), "V = 1 keeps the wave bits on top");
     template <int X>
     static constexpr int wt(int k) {
         return k < H ? MAPS.m[X].w[k] : CH << (k - H);
@@ -253,7 +291,7 @@ struct NttGeo {
     static constexpr bool banks_distinct(int p) {
         bool seen[32] = {};
         for (int l = 0; l < (1 << GB); ++l) {
-            const int b = at<X>(((l >> lo(p)) << (lo(p) + e)) | (l & ((1 << lo(p)) - 1))) & ((1 << GB) - 1);
+            const int b = at<X>(geo_base(LOG, e, p, l, V)) & ((1 << GB) - 1);
             if (seen[b]) return false;
             seen[b] = true;
         }
@@ -262,15 +300,15 @@ struct NttGeo {
     // gfx950 b128 conflict check of exchange map X (see make_b128_map): the writes of
     // the written layout hit 8 distinct bank quads per 8-lane group, the reads of the
     // read layout 16 distinct quads per read group, in both directions
+    // (max_way: the largest number of a group's lanes allowed on one bank quad)
     template <int X>
-    static constexpr bool b128_layout_ok(int p, bool write) {
+    static constexpr bool b128_layout_ok(int p, bool write, int max_way = 1) {
         for (int g = 0; g < (write ? 8 : 4); ++g) {
-            bool seen[16] = {};
+            int seen[16] = {};
             for (int l = 0; l < 64; ++l) {
                 if ((write ? l >> 3 : b128_rgroup(l)) != g) continue;
-                const int b = at<X>(((l >> lo(p)) << (lo(p) + e)) | (l & ((1 << lo(p)) - 1))) & (write ? 7 : 15);
-                if (seen[b]) return false;
-                seen[b] = true;
+                const int b = at<X>(geo_base(LOG, e, p, l, V)) & (write ? 7 : 15);
+                if (++seen[b] > max_way) return false;
             }
         }
         return true;
@@ -289,16 +327,24 @@ struct NttGeo {
     template <int X>
     static constexpr bool b128_exchange_ok() {
         const int xt = X + 1 < NPH ? X + 1 : X;
-        return MAPS.m[X].span > 0 && map_injective<X>() && b128_layout_ok<X>(X, true) && b128_layout_ok<X>(xt, false) &&
-               b128_layout_ok<X>(xt, true) && b128_layout_ok<X>(X, false);
+        const int xf = b128_mac_only(X, NPH, V) ? xt : X;
+        const int rw = b128_relaxed_read(X, V);
+        return MAPS.m[X].span > 0 && map_injective<X>() && b128_layout_ok<X>(xf, true) &&
+               b128_layout_ok<X>(xt, false, xt == rw ? 2 : 1) && b128_layout_ok<X>(xt, true) &&
+               b128_layout_ok<X>(xf, false, xf == rw ? 2 : 1);
     }
     // element m of lane tl in phase p: idx = base(tl) | moff(m), disjoint bits,
     // so at(idx) = at(base) + at(moff): every address is one per-lane register
     // plus a compile-time immediate.
     template <int p>
     __device__ static __forceinline__ int base(int tl) {
-        constexpr int L = lo(p);
-        return ((tl >> L) << (L + e)) | (tl & ((1 << L) - 1));
+        if constexpr (V == 1 && p >= 3) {  // lane bits 0..3 -> index 4, 5, 7, 6
+            return ((tl & 3) << 4) | ((tl & 4) << 5) | ((tl & 8) << 3) | (((tl >> 4) & 3) << (p == 3 ? 0 : 2)) |
+                   ((tl >> 6) << 8);
+        } else {
+            constexpr int L = lo(p);
+            return ((tl >> L) << (L + e)) | (tl & ((1 << L) - 1));
+        }
     }
     template <int p>
     static constexpr int moff(int m) { return m << lo(p); }

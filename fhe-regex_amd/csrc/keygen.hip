@@ -163,16 +163,16 @@ __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict_
     const double scale = 1.0 / (double)M;  // 2^-LOG, exact
     for (int idx = tid; idx < M; idx += 256) {
         {  // E = 8
-            constexpr int E = 8, e = 3, T = M / E;
+            constexpr int E = 8, e = 3, T = M / E, LAST = (LOG + e - 1) / e - 1;
             const int m = idx / T, tl = idx % T;
-            const int slot = (((tl >> L8) << (L8 + e)) | (tl & ((1 << L8) - 1))) + (m << L8);
+            const int slot = geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << L8);
             const double2 v = z[slot];
             out8[p * M + idx] = make_double2(v.x * scale, v.y * scale);
         }
         {  // E = 4
-            constexpr int E = 4, e = 2, T = M / E;
+            constexpr int E = 4, e = 2, T = M / E, LAST = (LOG + e - 1) / e - 1;
             const int m = idx / T, tl = idx % T;
-            const int slot = (((tl >> L4) << (L4 + e)) | (tl & ((1 << L4) - 1))) + (m << L4);
+            const int slot = geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << L4);
             const double2 v = z[slot];
             out4[p * M + idx] = make_double2(v.x * scale, v.y * scale);
         }
