@@ -1,23 +1,38 @@
 """Benchmark: TFHE gate-bootstraps/sec and end-to-end match time of /abc/ on
 256-char content (BASELINE.json metric), on MI355X through the C-ABI.
 
-One step = one homomorphic has_match of /abc/ over the rank's 256-char shard of
-synthetic printable-ASCII content (real encryptions under the reference's fixture
-client key, "abc" planted at global position 200): parse -> enumerate ->
-record -> lower -> level-scheduled KS + blind-rotation launches -> result.
-Ranks shard start offsets (weak scaling: 256 starts per GPU); for N > 1 the
-per-rank boolean results are all-gathered over RCCL and OR-reduced with one
-threshold bootstrap on rank 0 (inside the timed step).
+One step = one homomorphic has_match of the workload's pattern over its
+content (real encryptions under the reference's fixture client key, inputs
+resident in HBM): parse -> enumerate -> record -> lower -> level-scheduled
+KS + blind-rotation launches -> result (repeat matches replay the cached plan).
 
-value = gate bootstraps (blind rotations) executed by all ranks per second of
-wall time (multi-value bootstrapping lets one rotation serve several LUTs: the
-LUT-output rate is reported beside it, never as the value);
-ms_per_step = end-to-end match time.  roofline: blind-rotation kernel, HIP
-events on the library's stream over the timed region, algorithmic bytes per
-bootstrap n*(k+1)^2*l*N*8.  cpu_baseline: the CPU restatement
-(oracle/, "port") timed on this host on a bounded sample.
+Workloads (--workload; BASELINE.json configs): metric = /abc/ on 256 printable
+chars with "abc" at 200; config2 = /abc/ on 64 chars (run it with --params
+k2n1024, BASELINE's "N=1024"); config3 = /^[a-z0-9]+$/ on 256 chars (grammar
+extension: the reference returns Err); config4 = /the/i on 1024 chars;
+config5 = /^a{2,8}(bc|de)+[^xyz]$/ on 512 chars (state-merging engine).
+
+N > 1 (one process per GPU, torch.distributed over RCCL):
+  --scaling strong (default): the named content length is fixed and ONE match
+    is split across the ranks level by level (fheregex.run_sharded over the
+    fr_shard_* C-ABI): each rank runs a contiguous slice of every level's
+    rotation jobs and the level's output LWEs are all-gathered device to device
+    (RCCL all_gather_into_tensor); rank 0 runs the last level.
+  --scaling weak: --chars start offsets per GPU (content grows with N); each
+    rank matches its start range on the content window those starts read, the
+    per-rank booleans are all-gathered device to device and OR-ed on rank 0.
+
+value = blind rotations executed by all ranks per second of wall time (one
+rotation can serve several LUTs: multi-value bootstrapping; the LUT-output
+rate is reported beside it, never as the value); ms_per_step = match time.
+roofline: the blind-rotation kernel on rank 0, HIP events on the library's
+stream over the timed region; algorithmic bytes per bootstrap
+n*(k+1)^2*l*N*8; traffic / compute from the rocprofv3 PMC pass
+of this kernel source (tools/profile.sh -> tools/pmc_summary.py).
+cpu_baseline: the CPU restatement (oracle/, "port") timed on this host.
 """
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -32,7 +47,18 @@ import fheregex as F  # noqa: E402
 
 METRIC = "TFHE gate-bootstraps/sec; end-to-end match time for /abc/ on 256-char content"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# measured wave64 v_fma_f64 issue: 54 lane-ops per CU-clock = 0.84 VALU wave-instructions
+# per CU-clock (tools/ubench_f64.hip, profiles/r01/ubench_f64.log)
+VALU_F64_PEAK = 54.0 / 64.0
 SERVER_KEY_SEED = 42
+CONFIG5 = "/^a{2,8}(bc|de)+[^xyz]$/"
+WORKLOADS = {
+    "metric": dict(pattern="/abc/", chars=256, content="printable"),
+    "config2": dict(pattern="/abc/", chars=64, content="printable"),
+    "config3": dict(pattern="/^[a-z0-9]+$/", chars=256, content="alnum", grammar=F.GRAMMAR_EXT),
+    "config4": dict(pattern="/the/i", chars=1024, content="letters"),
+    "config5": dict(pattern=CONFIG5, chars=512, content="config5"),
+}
 
 
 def algorithmic_bytes_per_pbs(p) -> int:
@@ -40,40 +66,122 @@ def algorithmic_bytes_per_pbs(p) -> int:
     return p.n * (p.k + 1) ** 2 * p.pbs_level * p.N * 8
 
 
-def cpu_baseline(params_name: str, sample: int, ring: int):
-    """Time the oracle (CPU restatement, test infrastructure) on this host, on
-    the same ring as the GPU run."""
+def make_content(kind: str, L: int) -> bytes:
+    """Seeded synthetic content of the workload (every workload matches)."""
+    rng = np.random.default_rng(0)
+    if kind == "printable":
+        c = bytearray(rng.integers(0x20, 0x7F, L, dtype=np.uint8).tobytes())
+        at = 200 if L >= 256 else L // 4
+        c[at:at + 3] = b"abc"
+        return bytes(c)
+    if kind == "alnum":
+        alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz0123456789", dtype=np.uint8)
+        return bytes(rng.choice(alpha, L))
+    if kind == "letters":  # /the/i planted once at 700 (or L*2/3), no other case variant of "the"
+        alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
+        s = bytearray(rng.choice(alpha, L))
+        for i in range(L - 2):
+            if bytes(s[i:i + 3]).lower() == b"the":
+                s[i + 2] = ord("x")
+        at = 700 if L >= 1024 else (2 * L) // 3
+        s[at:at + 3] = b"ThE"
+        return bytes(s)
+    if kind == "config5":  # a{3}(bc|de)*f: matches /^a{2,8}(bc|de)+[^xyz]$/ for even L
+        import random
+        r5 = random.Random(5)
+        c = ("aaa" + "".join(r5.choice(["bc", "de"]) for _ in range((L - 4) // 2)) + "f").encode()
+        assert len(c) == L, "config5 content needs an even length"
+        return c
+    raise ValueError(kind)
+
+
+def content_window(L: int, pattern: str, lo: int, hi: int, grammar: int, engine: int, lowering: int):
+    """[wlo, whi): the content positions the circuit of starts [lo, hi) reads
+    (from the lowered schedule, so no --halo guess)."""
+    S = F.schedule_match(L, pattern, lo, hi, lowering=lowering, engine=engine, grammar=grammar)
+    pos = [(-1 - j.in_ref[q]) // 4 for j in S.jobs for q in range(j.n_in) if j.in_ref[q] < 0]
+    return (min(pos), max(pos) + 1) if pos else (lo, lo)
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int, lowering: int,
+                 sample: int, match_max_jobs: int):
+    """The oracle (oracle/: the CPU restatement of this path, test infrastructure)
+    timed on this host: 1-thread and all-threads gate-bootstrap rates
+    on a sample of eq-nibble gates, and the CPU end-to-end match of the workload on
+    the same lowered schedule (the reference's serial fold, engine.rs:22-35)."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_ffi as of
 
-    key = of.load_fixture_key()
-    k, N = (1, 2048) if params_name == "k1n2048" else (2, 1024)
-    O = of.Oracle(key, seed=SERVER_KEY_SEED, k=k, N=N, ring=ring)
-    threads = of.lib().or_num_threads()
-    blocks = O.encrypt_blocks([i % 4 for i in range(2 * sample)], seed=5)
+    O = of.Oracle(of.load_fixture_key(), seed=SERVER_KEY_SEED, k=params.k, N=params.N, ring=params.ring)
+    threads = O.num_threads()
     lut = [int(v == 1) for v in range(16)]
+    blocks = O.encrypt_blocks([i % 4 for i in range(2 * sample)], seed=5)
     gates = [([(2 * i, 1), (2 * i + 1, 4)], 0, lut) for i in range(sample)]
+    O.set_threads(1)
+    n1 = max(4, sample // 48)
+    t0 = time.perf_counter()
+    O.gates(gates[:n1], blocks)
+    t1 = time.perf_counter() - t0
+    O.set_threads(threads)
     t0 = time.perf_counter()
     O.gates(gates, blocks)
-    dt = time.perf_counter() - t0
+    tall = time.perf_counter() - t0
+    rate_all = sample / tall
+    S = F.schedule_match(len(content), pattern, lowering=lowering, engine=engine, grammar=grammar)
+    match = {"jobs": len(S.jobs), "levels": len(S.level_off) - 1}
+    if len(S.jobs) <= match_max_jobs:
+        ct = O.encrypt_str(content, seed=7)
+        t0 = time.perf_counter()
+        res = O.run_schedule(S, ct)
+        match["ms"] = (time.perf_counter() - t0) * 1e3
+        match["result_decrypted"] = int(O.decode16(res)[0])
+        match["how"] = "measured: every job of the lowered schedule on the CPU, level by level"
+    else:
+        match["ms"] = len(S.jobs) / rate_all * 1e3
+        match["how"] = f"estimated: jobs / all-threads rate (more than {match_max_jobs} jobs)"
+    ring = "f64 FFT" if params.ring == F.RING_FFT else "RNS NTT"
     return {
-        "value": sample / dt,
+        "value": rate_all,
         "unit": "gate-bootstraps/s",
         "cores": threads,
         "kind": "port",
-        "sample": f"{sample} eq-nibble gate bootstraps (lincomb+KS+BR+SE, {params_name}, "
-                  f"{'f64 FFT' if ring == of.RING_FFT else 'RNS NTT'} ring) on the fixture key, "
-                  f"{threads} OpenMP threads, {dt:.1f} s",
+        "label": "build CPU restatement (oracle/, unoptimised, not tfhe-rs): a lower bound on a CPU path",
+        "value_1t": n1 / t1,
+        "value_all": rate_all,
+        "nproc": os.cpu_count(),
+        "model": cpu_model(),
+        "match_ms": match["ms"],
+        "match": match,
+        "sample": f"{sample} eq-nibble gate bootstraps (lincomb+KS+BR+SE, k={params.k} N={params.N}, {ring} ring) "
+                  f"on {threads} OpenMP threads in {tall:.1f} s; {n1} on 1 thread in {t1:.1f} s",
     }
 
 
-def load_traffic(path):
+def pmc_figures(params, path: str):
+    """traffic (HBM bytes per BR launch) and the VALU issue rate of the BR kernel
+    from tools/pmc_summary.py's JSON; stale when the kernel source changed since."""
     try:
         with open(path) as f:
             d = json.load(f)
-        return d.get("hbm_bytes_per_launch"), d
     except (OSError, ValueError):
-        return None, None
+        return None
+    if d.get("ring", "rns") != ("fft" if params.ring == F.RING_FFT else "rns") or d.get("k", 1) != params.k:
+        return None
+    src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
+    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16] if os.path.exists(src) else None
+    return {"traffic": d.get("hbm_bytes_per_launch"), "valu_per_cu_clk": d.get("valu_per_cu_clk"),
+            "source": os.path.relpath(path, REPO), "stale": d.get("kernel_sha") != sha}
 
 
 def main():
@@ -81,23 +189,33 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--chars", type=int, default=256, help="content chars (start offsets) per GPU")
-    ap.add_argument("--pattern", default="/abc/")
+    ap.add_argument("--workload", default="metric", choices=sorted(WORKLOADS))
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="N>1: strong = the workload's content split across ranks (one match, level-sharded); "
+                         "weak = --chars start offsets per GPU")
+    ap.add_argument("--chars", type=int, default=0, help="content chars (strong: total; weak: per GPU); 0: workload's")
+    ap.add_argument("--pattern", default="", help="override the workload's pattern")
+    ap.add_argument("--content", default="", choices=["", "printable", "alnum", "letters", "config5"])
     ap.add_argument("--params", default="k1n2048", choices=["k1n2048", "k2n1024"])
-    ap.add_argument("--ring", default="auto", choices=["auto", "fft", "rns"],
-                    help="blind-rotation ring: f64-FFT torus (default for k1n2048) or the RNS NTT ring")
-    ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"],
-                    help="regex evaluation: the reference's enumeration, state merging, or auto")
-    ap.add_argument("--content", default="printable", choices=["printable", "config5"],
-                    help="printable: seeded ASCII with 'abc' at 200; config5: a{3}(bc|de)*f (BASELINE config 5)")
+    ap.add_argument("--ring", default="auto", choices=["auto", "fft", "rns"])
+    ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"])
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
-    ap.add_argument("--cpu-sample", type=int, default=384, help="gate bootstraps in the CPU baseline sample (0: skip)")
-    ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated kernel-throughput probe (0: skip)")
-    ap.add_argument("--halo", type=int, default=2, help="chars read past the last start (pattern span - 1; 2 for /abc/)")
+    ap.add_argument("--cpu-sample", type=int, default=384, help="gates in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
+    ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated throughput probe (0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="collective backend for N>1 (nccl = RCCL over xGMI; gloo only to rehearse several ranks on one GPU)")
+                    help="N>1 collectives (nccl = RCCL over xGMI; gloo only to rehearse ranks sharing one GPU)")
     ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
+    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "r02", "pmc_summary.json"),
+                    help="PMC summary of the BR kernel (tools/pmc_summary.py)")
     args = ap.parse_args()
+
+    W = WORKLOADS[args.workload]
+    pattern = args.pattern or W["pattern"]
+    kind = args.content or W["content"]
+    grammar = W.get("grammar", F.GRAMMAR_REFERENCE)
+    engine = {"auto": F.ENGINE_AUTO, "enumerate": F.ENGINE_ENUMERATE, "merged": F.ENGINE_MERGED}[args.engine]
+    lowering = F.LOWER_THRESHOLD if args.lowering == "threshold" else F.LOWER_FAITHFUL
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -105,15 +223,15 @@ def main():
     import torch
 
     dist = None
-    # one process per GPU; ranks beyond the visible devices (a gloo rehearsal on
-    # a one-GPU box) share devices round-robin
+    # one process per GPU; ranks beyond the visible devices (a gloo rehearsal on a
+    # one-GPU box) share devices round-robin
     device = local_rank % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(device)
         dist.init_process_group(args.dist_backend)
-    coll_dev = "cuda" if args.dist_backend == "nccl" else "cpu"
+    coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
 
     def barrier():
         if dist is not None:
@@ -129,107 +247,109 @@ def main():
     t_key = time.perf_counter()
     ctx.gen_server_key(SERVER_KEY_SEED)  # same seed on every rank: identical keys, no broadcast needed
     t_key = time.perf_counter() - t_key
-    ctx.set_lowering(F.LOWER_THRESHOLD if args.lowering == "threshold" else F.LOWER_FAITHFUL)
-    ctx.set_engine({"auto": F.ENGINE_AUTO, "enumerate": F.ENGINE_ENUMERATE, "merged": F.ENGINE_MERGED}[args.engine])
+    ctx.set_lowering(lowering)
+    ctx.set_engine(engine)
+    ctx.set_grammar(grammar)
 
-    # synthetic content: printable ASCII, "abc" planted at global position 200
-    L = args.chars * world
-    rng = np.random.default_rng(0)
-    content = bytearray(rng.integers(0x20, 0x7F, L, dtype=np.uint8).tobytes())
-    content[200:203] = b"abc"
-    content = bytes(content)
-    if args.content == "config5":  # matches /^a{2,8}(bc|de)+[^xyz]$/ when L is even
-        import random
-        r5 = random.Random(5)
-        content = ("aaa" + "".join(r5.choice(["bc", "de"]) for _ in range((L - 4) // 2)) + "f").encode()
-        assert len(content) == L, "config5 content needs an even length"
-        args.halo = L  # anchored pattern: a branch reads to the end of the content
-    lo, hi = F.shard_starts(L, world, rank)  # this rank's start offsets
-    win_hi = min(L, hi + args.halo)          # + halo: chars a branch may read past its start
-    msgs = [(c >> (2 * b)) & 3 for c in content[lo:win_hi] for b in range(4)]
-    blocks = ctx.encrypt_blocks(msgs, seed=7, first_block=4 * lo).reshape(win_hi - lo, 4, ctx.lwe_len)
+    chars = args.chars or W["chars"]
+    strong = args.scaling == "strong" or world == 1
+    L = chars if strong else chars * world
+    content = make_content(kind, L)
+    expected = F.plain_match(content, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+    # content each rank holds: strong = all of it; weak = the window its starts read
+    if strong:
+        lo, hi, wlo, whi = 0, L, 0, L
+    else:
+        lo, hi = F.shard_starts(L, world, rank)
+        wlo, whi = content_window(L, pattern, lo, hi, grammar, engine, lowering)
     handles = [F.NULL_CT] * L
-    for i, h in enumerate(ctx.upload_radix(blocks)):
-        handles[lo + i] = h
+    if whi > wlo:
+        msgs = [(c >> (2 * b)) & 3 for c in content[wlo:whi] for b in range(4)]
+        blocks = ctx.encrypt_blocks(msgs, seed=7, first_block=4 * wlo).reshape(whi - wlo, 4, ctx.lwe_len)
+        for i, h in enumerate(ctx.upload_radix(blocks)):
+            handles[wlo + i] = h
+
+    plan = None
+    if world > 1:
+        gather = F.torch_all_gather()
+        if strong:
+            plan = F.ShardPlan(ctx, handles, pattern)
 
     def step():
-        out, st = ctx.has_match(handles, args.pattern, lo, hi)
-        final_pbs = 0
-        if world > 1:
-            lwe = ctx.download_radix(out)[0]
-            t = torch.from_numpy(lwe.view(np.int64)).to(coll_dev)
-            parts = [torch.empty_like(t) for _ in range(world)]
-            dist.all_gather(parts, t)
+        """one match; returns (result handle on rank 0 or None, rotations run by this rank)"""
+        if world == 1:
+            out, st = ctx.has_match(handles, pattern)
+            return out, st.blind_rotations, st
+        if strong:
+            F.run_sharded(plan, world, rank, gather)
+            mine = sum(len(range(*F.job_slice(plan.jobs(l), world, rank))) for l in range(plan.levels - 1))
             if rank == 0:
-                arr = np.stack([p.cpu().numpy().view(np.uint64) for p in parts])
-                bh = ctx.upload_bool(arr)
-                res = ctx.or_many(bh)
-                final_pbs = 1 if world <= 15 else -1
-                for h in bh:
-                    ctx.release(h)
-                ctx.release(out)
-                out = res
-        return out, st, final_pbs
+                out, st = plan.finish()
+                return out, mine + plan.jobs(plan.levels - 1), st
+            return None, mine, plan.stats
+        out, st = ctx.has_match(handles, pattern, lo, hi)
+        buf = torch.empty(ctx.lwe_len, dtype=torch.int64, device=f"cuda:{device}")
+        ctx.export_bool_device([out], buf.data_ptr())
+        ctx.release(out)
+        recv = torch.cat(gather(buf))  # [world * lwe_len] on this GPU
+        torch.cuda.synchronize()
+        if rank != 0:
+            return None, st.blind_rotations, st
+        parts = ctx.import_bool_device(recv.data_ptr(), world)
+        res = ctx.or_many(parts)
+        for h in parts:
+            ctx.release(h)
+        return res, st.blind_rotations + (1 if world <= 15 else 2), st
 
     first_call = None
     for _ in range(args.warmup):
-        o, st0, _ = step()
+        o, _, st0 = step()
         if first_call is None:  # cold call: parse, record, lower, compile, plan upload
             first_call = {"host_ms": st0.host_ms, "device_ms": st0.device_ms, "plan_cached": st0.plan_cached}
-        ctx.release(o)
+        if o is not None:
+            ctx.release(o)
 
     ctx.set_profiling(True)
+    t_before = ctx.device_timers()
     barrier()
     t0 = time.perf_counter()
-    pbs_local = 0
     rot_local = 0
-    br_ms = 0.0
-    br_launches = 0
-    br_gates = 0
     host_ms = 0.0
-    levels = 0
-    final_pbs_total = 0
     out = None
+    st = None
     for i in range(args.steps):
-        o, st, fp = step()
-        pbs_local += st.pbs
-        rot_local += st.blind_rotations
-        br_ms += st.br_kernel_ms
-        br_launches += st.br_launches
-        br_gates += st.br_gates
-        host_ms += st.host_ms
-        levels = st.levels
-        final_pbs_total += max(fp, 0)
-        if i + 1 < args.steps:
-            ctx.release(o)
-        else:
-            out = o
+        o, rot, st = step()
+        rot_local += rot
+        host_ms += st.host_ms if world == 1 else 0.0
+        if o is not None:
+            if i + 1 < args.steps:
+                ctx.release(o)
+            else:
+                out = o
     barrier()
     elapsed = time.perf_counter() - t0
+    t_after = ctx.device_timers()
     ctx.set_profiling(False)
 
     if dist is not None:
-        tt = torch.tensor([elapsed, float(pbs_local + final_pbs_total), float(rot_local + final_pbs_total)],
-                          dtype=torch.float64, device=coll_dev)
+        tt = torch.tensor([elapsed, float(rot_local)], dtype=torch.float64, device=coll_dev)
         mx = tt.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
-        elapsed, total_pbs, total_rot = float(mx[0]), float(tt[1]), float(tt[2])
+        elapsed, total_rot = float(mx[0]), float(tt[1])
     else:
-        total_pbs = float(pbs_local + final_pbs_total)
-        total_rot = float(rot_local + final_pbs_total)
+        total_rot = float(rot_local)
 
     result = None
     if rank == 0:
         result = ctx.decrypt_radix(ctx.download_radix(out))
-        expected = 1 if 200 < L - 2 else 0
         if result != expected:
             print(f"WARNING: decrypted result {result} != expected {expected}", file=sys.stderr)
 
-    # saturated kernel-throughput probe: one big batch of independent PBS
     kernel = None
     if args.saturate and rank == 0:
-        hs = [handles[lo + (i % (win_hi - lo))] for i in range(args.saturate)]
+        src = [h for h in handles if h != F.NULL_CT]
+        hs = [src[i % len(src)] for i in range(args.saturate)]
         br_sat, tot_sat = ctx.dev_bench_pbs(hs, 2)
         kernel = {"gates_per_launch": args.saturate, "br_ms_per_launch": br_sat / 2,
                   "pbs_per_s": 2 * args.saturate / (tot_sat / 1e3),
@@ -237,26 +357,39 @@ def main():
 
     probe = None
     if args.probe and rank == 0:
+        src = [h for h in handles if h != F.NULL_CT]
         probe = {}
         for cnt in [int(x) for x in args.probe.split(",")]:
-            hs = [handles[lo + (i % (win_hi - lo))] for i in range(cnt)]
+            hs = [src[i % len(src)] for i in range(cnt)]
             br_p, tot_p = ctx.dev_bench_pbs(hs, 2)
             probe[cnt] = {"br_ms": br_p / 2, "total_ms": tot_p / 2}
 
     if rank != 0:
+        if plan is not None:
+            plan.free()
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
         return
 
     bpp = algorithmic_bytes_per_pbs(params)
+    br_ms = t_after["br_ms"] - t_before["br_ms"]
+    br_launches = t_after["br_launches"] - t_before["br_launches"]
+    br_gates = t_after["br_gates"] - t_before["br_gates"]
     achieved_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
-    traffic, tinfo = load_traffic(os.path.join(REPO, "profiles", "r01", "pmc_summary.json"))
-    if tinfo is not None and tinfo.get("ring", "rns") != ("fft" if params.ring == F.RING_FFT else "rns"):
-        traffic = None  # the PMC summary was measured on the other ring
-    cpu = cpu_baseline(args.params, args.cpu_sample, params.ring) if args.cpu_sample > 0 and world == 1 else None
+    pmc = pmc_figures(params, args.pmc)
+    cpu = None
+    if args.cpu_sample > 0 and world == 1:
+        cpu = cpu_baseline(params, content, pattern, grammar, engine, lowering, args.cpu_sample,
+                           args.cpu_match_max_jobs)
     ms_per_step = elapsed / args.steps * 1e3
     ring_name = "fft" if params.ring == F.RING_FFT else "rns"
+    if world == 1:
+        par = "single GPU"
+    elif strong:
+        par = f"level-sharded x{world} (job slices per level, RCCL all_gather of each level's LWEs)"
+    else:
+        par = f"start-offset shards x{world} (RCCL all_gather of the per-rank booleans, OR on rank 0)"
     line = {
         "metric": METRIC,
         "value": total_rot / elapsed,
@@ -266,23 +399,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u64",
-        "data": "synthetic: seeded printable ASCII, real encryptions under the reference fixture client key",
-        "config": {"workload": f"{args.pattern} contains-match, {args.chars} chars per GPU (start-offset shards)",
+        "data": "synthetic: seeded content, real encryptions under the reference fixture client key",
+        "config": {"workload": f"{args.workload}: {pattern} on {L} chars" + ("" if strong else f" ({chars} per GPU)"),
                    "content_chars": L, "params": args.params, "ring": ring_name, "lowering": args.lowering,
-                   "engine": args.engine,
-                   "content": args.content,
-                   "parallelism": f"start-offset shards x{world}"},
+                   "engine": args.engine, "content": kind, "scaling": "strong" if strong else "weak",
+                   "parallelism": par},
         "match_ms": ms_per_step,
         "blind_rotations_per_match": total_rot / args.steps,
-        "lut_outputs_per_match": total_pbs / args.steps,
-        "lut_outputs_per_s": total_pbs / elapsed,
-        "levels": levels,
-        "host_ms_per_match": host_ms / args.steps,
+        "lut_outputs_per_match": float(st.pbs) if world == 1 or strong else None,
+        "levels": st.levels,
+        "host_ms_per_match": host_ms / args.steps if world == 1 else None,
         "first_call": first_call,
         "result_decrypted": result,
+        "result_expected": expected,
         "keygen_s": t_key,
         "roofline": {
             "bound": "hbm",
@@ -290,18 +422,31 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": achieved_gbs / HBM_PEAK_GBS,
-            "traffic": traffic,
+            "traffic": pmc["traffic"] if pmc else None,
             "kernel": "k_blind_rotate_fft" if params.ring == F.RING_FFT else "k_blind_rotate",
+            "achieved_is": "algorithmic GGSW bytes (n (k+1)^2 l N 8 per bootstrap) / average BR launch time",
             "bytes_per_pbs": bpp,
             "br_launches": br_launches,
             "br_avg_ms": br_ms / max(br_launches, 1),
             "br_gates_per_launch": br_gates / max(br_launches, 1),
+            "compute": None if not pmc or pmc.get("valu_per_cu_clk") is None else {
+                "bound": "valu",
+                "achieved": pmc["valu_per_cu_clk"],
+                "peak": VALU_F64_PEAK,
+                "unit": "VALU wave-instructions per active-CU clock",
+                "frac": pmc["valu_per_cu_clk"] / VALU_F64_PEAK,
+                "peak_is": "measured wave64 v_fma_f64 issue rate (profiles/r01/ubench_f64.log)",
+            },
+            "pmc_source": pmc["source"] if pmc else None,
+            "pmc_stale": pmc["stale"] if pmc else None,
         },
         "kernel_saturated": kernel,
         "latency_probe": probe,
         "cpu_baseline": cpu,
     }
     print(json.dumps(line))
+    if plan is not None:
+        plan.free()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -127,12 +127,126 @@ namespace fr {
 constexpr int MV_MAX_NORM2 = 8;
 
 // ---------------------------------------------------------------- executor
-// A PBS program whose negative sources refer to blocks of `inputs` (input q =
-// pos q: src = -(1 + q*4 + blk)) compiles to a Plan: one DevGate batch per
-// dependency level, every input resolved to an arena slot (trivial blocks folded
-// into the offset), small-norm LUTs on the same linear combination merged into one
-// multi-value rotation.  Every gate is validated before any slot is allocated, and
-// the slots allocated so far are returned if compilation throws.
+// A PBS program whose negative sources refer to content blocks (input q = pos q:
+// src = -(1 + q*4 + blk)) becomes a Schedule: its rotation jobs by dependency level,
+// small-norm LUTs on the same linear combination merged into one multi-value job.
+// Job references are abstract: in_slot[q] >= 0 is the output of program gate
+// in_slot[q], in_slot[q] < 0 content block -1 - in_slot[q]; out_slot[f] is a program
+// gate.  Trivial content blocks are folded into the offset.  Building a schedule
+// validates every gate and allocates nothing; a host-only context builds the same
+// schedule (fr_schedule_match) as the device plan, which maps the references to
+// arena slots (compile_plan).
+struct Schedule {
+    std::vector<DevGate> jobs;      // levels concatenated
+    std::vector<size_t> level_off;  // level l (0-based): jobs [level_off[l], level_off[l+1])
+    size_t n_gates = 0;
+    uint64_t levels = 0, max_width = 0;
+};
+
+// block(cb, &key, &triv): false if content block cb is trivial (its value in triv),
+// else key identifies the block's ciphertext (the multi-value merge compares keys)
+template <class Block>
+static Schedule build_schedule(const std::vector<PGate>& gates, size_t n_content, bool multi_value, Block&& block) {
+    // 1. validation: topological order, input range, fan-in, offsets
+    std::vector<int> level(gates.size(), 0);
+    int maxl = 0;
+    for (size_t g = 0; g < gates.size(); ++g) {
+        const PGate& G = gates[g];
+        int l = 0, nin = 0, off = G.offset;
+        for (auto& in : G.ins) {
+            if (in.src >= 0) {
+                if ((size_t)in.src >= g) throw Error(FR_ERR_INVALID, "gate program is not topologically ordered");
+                l = std::max(l, level[in.src]);
+                ++nin;
+                continue;
+            }
+            const int cb = -in.src - 1;
+            if ((size_t)(cb / 4) >= n_content) throw Error(FR_ERR_INVALID, "gate input out of range");
+            int key = 0, triv = 0;
+            if (block(cb, key, triv)) ++nin;
+            else off += 2 * in.w * triv;
+        }
+        if (nin > 16) throw Error(FR_ERR_INVALID, "gate fan-in > 16");
+        if (G.kind != GATE_SIGN && (off & 1)) throw Error(FR_ERR_INVALID, "LUT gate with a half-integral offset");
+        level[g] = l + 1;
+        maxl = std::max(maxl, l + 1);
+    }
+    std::vector<std::vector<int>> by_level(maxl + 1);
+    for (size_t g = 0; g < gates.size(); ++g) by_level[level[g]].push_back((int)g);
+    // 2. jobs, level by level
+    Schedule S;
+    S.n_gates = gates.size();
+    S.level_off.push_back(0);
+    for (int l = 1; l <= maxl; ++l) {
+        const size_t first = S.jobs.size();
+        // input signature -> open job index
+        std::map<std::vector<int32_t>, size_t> open_job;
+        for (int g : by_level[l]) {
+            const PGate& G = gates[g];
+            DevGate d;
+            std::memset(&d, 0, sizeof d);
+            int off = G.offset, nin = 0;
+            std::vector<int32_t> sig;
+            for (auto& in : G.ins) {
+                int ref, key;
+                if (in.src >= 0) {
+                    ref = in.src;
+                    key = in.src;
+                } else {
+                    const int cb = -in.src - 1;
+                    int triv = 0;
+                    if (!block(cb, key, triv)) {
+                        off += 2 * in.w * triv;  // offsets are in units of Delta/2
+                        continue;
+                    }
+                    ref = -1 - cb;
+                    key = -1 - key;
+                }
+                d.in_slot[nin] = ref;
+                d.in_w[nin] = in.w;
+                sig.push_back(key);
+                sig.push_back(in.w);
+                ++nin;
+            }
+            d.n_in = nin;
+            d.offset = off;
+            if (G.kind == GATE_SIGN) {
+                d.n_out = 1;
+                d.direct = JOB_SIGN;
+                d.out_slot[0] = g;
+                S.jobs.push_back(d);
+                continue;
+            }
+            const bool small = lut_w_norm2(G.lut) <= MV_MAX_NORM2;
+            if (small && multi_value) {
+                sig.push_back(nin);
+                sig.push_back(off);
+                auto it = open_job.find(sig);
+                if (it != open_job.end() && S.jobs[it->second].n_out < MAX_OUT) {
+                    DevGate& J = S.jobs[it->second];
+                    std::memcpy(J.lut[J.n_out], G.lut, 16);
+                    J.out_slot[J.n_out] = g;
+                    J.n_out++;
+                    J.direct = JOB_MULTI;
+                    continue;
+                }
+                open_job[sig] = S.jobs.size();
+            }
+            std::memcpy(d.lut[0], G.lut, 16);
+            d.n_out = 1;
+            d.direct = JOB_DIRECT;
+            d.out_slot[0] = g;
+            S.jobs.push_back(d);
+        }
+        S.level_off.push_back(S.jobs.size());
+        S.max_width = std::max<uint64_t>(S.max_width, S.jobs.size() - first);
+    }
+    S.levels = (uint64_t)maxl;
+    return S;
+}
+
+// A device plan: the schedule with references mapped to arena slots (one slot per
+// program gate).  The slots allocated so far are returned if compilation throws.
 struct Plan {
     std::vector<DevGate> gates;     // levels concatenated
     std::vector<size_t> level_off;  // level l (0-based): gates [level_off[l], level_off[l+1])
@@ -149,34 +263,16 @@ static void free_plan_slots(Device& dev, std::vector<int>& slot) {
 static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs) {
     Device& dev = ctx->device();
     if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
-    // 1. validation (no allocation): topological order, input range, fan-in, offsets
-    std::vector<int> level(gates.size(), 0);
-    int maxl = 0;
-    for (size_t g = 0; g < gates.size(); ++g) {
-        const PGate& G = gates[g];
-        int l = 0, nin = 0, off = G.offset;
-        for (auto& in : G.ins) {
-            if (in.src >= 0) {
-                if ((size_t)in.src >= g) throw Error(FR_ERR_INVALID, "gate program is not topologically ordered");
-                l = std::max(l, level[in.src]);
-                ++nin;
-                continue;
-            }
-            const int cb = -in.src - 1;
-            const size_t q = (size_t)(cb / 4);
-            if (q >= inputs.size()) throw Error(FR_ERR_INVALID, "gate input out of range");
-            const Block& b = ctx->get(inputs[q]).b[cb % 4];
-            if (b.slot < 0) off += 2 * in.w * (int)b.triv;
-            else ++nin;
+    auto block_slot = [&](int cb) -> const Block& { return ctx->get(inputs[(size_t)(cb / 4)]).b[cb % 4]; };
+    Schedule S = build_schedule(gates, inputs.size(), ctx->multi_value, [&](int cb, int& key, int& triv) {
+        const Block& b = block_slot(cb);
+        if (b.slot < 0) {
+            triv = (int)b.triv;
+            return false;
         }
-        if (nin > 16) throw Error(FR_ERR_INVALID, "gate fan-in > 16");
-        if (G.kind != GATE_SIGN && (off & 1)) throw Error(FR_ERR_INVALID, "LUT gate with a half-integral offset");
-        level[g] = l + 1;
-        maxl = std::max(maxl, l + 1);
-    }
-    std::vector<std::vector<int>> by_level(maxl + 1);
-    for (size_t g = 0; g < gates.size(); ++g) by_level[level[g]].push_back((int)g);
-    // 2. allocation and batches
+        key = b.slot;
+        return true;
+    });
     Plan P;
     P.slot.assign(gates.size(), -1);
     struct Guard {
@@ -188,73 +284,17 @@ static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std
         }
     } guard{dev, P.slot};
     for (size_t g = 0; g < gates.size(); ++g) P.slot[g] = dev.alloc_slot();
-    P.level_off.push_back(0);
-    for (int l = 1; l <= maxl; ++l) {
-        const size_t first = P.gates.size();
-        // input signature -> open job index (multi-value bootstrapping merges
-        // small-norm LUTs that read the same linear combination)
-        std::map<std::vector<int32_t>, size_t> open_job;
-        for (int g : by_level[l]) {
-            const PGate& G = gates[g];
-            DevGate d;
-            std::memset(&d, 0, sizeof d);
-            int off = G.offset, nin = 0;
-            for (auto& in : G.ins) {
-                int s;
-                if (in.src >= 0) {
-                    s = P.slot[in.src];
-                } else {
-                    const int cb = -in.src - 1;
-                    const Block& b = ctx->get(inputs[(size_t)(cb / 4)]).b[cb % 4];
-                    if (b.slot < 0) {
-                        off += 2 * in.w * (int)b.triv;  // offsets are in units of Delta/2
-                        continue;
-                    }
-                    s = b.slot;
-                }
-                d.in_slot[nin] = s;
-                d.in_w[nin] = in.w;
-                ++nin;
-            }
-            d.n_in = nin;
-            d.offset = off;
-            if (G.kind == GATE_SIGN) {
-                d.n_out = 1;
-                d.direct = JOB_SIGN;
-                d.out_slot[0] = P.slot[g];
-                P.gates.push_back(d);
-                continue;
-            }
-            const bool small = lut_w_norm2(G.lut) <= MV_MAX_NORM2;
-            if (small && ctx->multi_value) {
-                std::vector<int32_t> sig{nin, off};
-                for (int q = 0; q < nin; ++q) {
-                    sig.push_back(d.in_slot[q]);
-                    sig.push_back(d.in_w[q]);
-                }
-                auto it = open_job.find(sig);
-                if (it != open_job.end() && P.gates[it->second].n_out < MAX_OUT) {
-                    DevGate& J = P.gates[it->second];
-                    std::memcpy(J.lut[J.n_out], G.lut, 16);
-                    J.out_slot[J.n_out] = P.slot[g];
-                    J.n_out++;
-                    J.direct = JOB_MULTI;
-                    continue;
-                }
-                open_job[sig] = P.gates.size();
-            }
-            std::memcpy(d.lut[0], G.lut, 16);
-            d.n_out = 1;
-            d.direct = JOB_DIRECT;
-            d.out_slot[0] = P.slot[g];
-            P.gates.push_back(d);
-        }
-        P.level_off.push_back(P.gates.size());
-        P.max_width = std::max<uint64_t>(P.max_width, P.gates.size() - first);
+    P.gates = std::move(S.jobs);
+    for (DevGate& d : P.gates) {
+        for (int q = 0; q < d.n_in; ++q)
+            d.in_slot[q] = d.in_slot[q] >= 0 ? P.slot[d.in_slot[q]] : block_slot(-1 - d.in_slot[q]).slot;
+        for (int f = 0; f < d.n_out; ++f) d.out_slot[f] = P.slot[d.out_slot[f]];
     }
+    P.level_off = std::move(S.level_off);
     P.pbs = gates.size();
     P.rotations = P.gates.size();
-    P.levels = (uint64_t)maxl;
+    P.levels = S.levels;
+    P.max_width = S.max_width;
     guard.armed = false;
     return P;
 }
@@ -1255,3 +1295,252 @@ uint64_t fr_debug_scalar(int32_t op, uint64_t x, uint64_t y) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ level-sharded matches
+// One match split across ranks (the reference folds ct_or over the
+// start offsets of engine.rs:15-35, and anchored patterns have a single start,
+// engine.rs:51-57): every rank compiles the same plan over its own copy of the
+// content, runs a contiguous slice of every level's rotation jobs, and all-gathers
+// the level's output LWEs device to device (fr_shard_export / fr_shard_import into
+// the caller's device buffers, e.g. RCCL all_gather); every rank then holds the
+// level's outputs and goes on to the next.  The plan keeps its slots and a device
+// copy of its batches, so repeat runs only enqueue.
+struct fr_shard {
+    fr::Plan plan;
+    int32_t out_gate = -1, out_w = 0, out_const = 0;
+    std::vector<std::vector<int>> out_slots;     // per level: output slots in job order
+    std::vector<std::vector<uint32_t>> out_off;  // per level: first output of each job (+ total)
+    fr_match_stats stats{};
+};
+
+namespace fr {
+static const std::vector<int>& shard_level_range(const fr_shard* sh, uint32_t level, uint32_t b, uint32_t e,
+                                                 uint32_t& first, uint32_t& count) {
+    if (level >= sh->out_off.size()) throw Error(FR_ERR_INVALID, "shard: level out of range");
+    const auto& off = sh->out_off[level];
+    if (b > e || e + 1 > off.size()) throw Error(FR_ERR_INVALID, "shard: job range out of range");
+    first = off[b];
+    count = off[e] - off[b];
+    return sh->out_slots[level];
+}
+}  // namespace fr
+
+int fr_shard_plan(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
+                  fr_shard** out, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && out && pattern && (content || !n) && lo <= hi);
+        Device& dev = ctx->device();
+        if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
+        const double t0 = now_ms();
+        ValueDag dag;
+        GrammarScope grammar(ctx->grammar);
+        Recorded rec = record_has_match_engine(dag, n, pattern, lo, hi, ctx->engine);
+        Program prog = lower(dag, rec.root, ctx->lowering);
+        for (auto& g : prog.gates)
+            for (auto& in : g.ins)
+                if (in.src < 0) {
+                    const size_t q = (size_t)((-in.src - 1) / 4);
+                    if (q >= n || content[q] == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
+                    if (ctx->get(content[q]).is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
+                }
+        auto sh = std::make_unique<fr_shard>();
+        sh->plan = compile_plan(ctx, prog.gates, std::vector<fr_ct>(content, content + n));
+        struct Guard {
+            fr_ctx* ctx;
+            fr_shard* sh;
+            ~Guard() {
+                if (sh) free_plan_slots(ctx->device(), sh->plan.slot);
+            }
+        } guard{ctx, sh.get()};
+        Plan& P = sh->plan;
+        P.d_gates = dev.upload_gates(P.gates.data(), P.gates.size());
+        sh->out_gate = prog.out_gate;
+        sh->out_w = prog.out_w;
+        sh->out_const = prog.out_const;
+        for (size_t l = 0; l + 1 < P.level_off.size(); ++l) {
+            std::vector<int> slots;
+            std::vector<uint32_t> off{0};
+            for (size_t j = P.level_off[l]; j < P.level_off[l + 1]; ++j) {
+                for (int f = 0; f < P.gates[j].n_out; ++f) slots.push_back(P.gates[j].out_slot[f]);
+                off.push_back((uint32_t)slots.size());
+            }
+            sh->out_slots.push_back(std::move(slots));
+            sh->out_off.push_back(std::move(off));
+        }
+        fr_match_stats& s = sh->stats;
+        s.ct_ops = rec.ct_ops;
+        s.cache_hits = rec.cache_hits;
+        s.n_branches = rec.n_branches;
+        s.pbs = P.pbs;
+        s.blind_rotations = P.rotations;
+        s.levels = P.levels;
+        s.max_level_width = P.max_width;
+        s.host_ms = now_ms() - t0;
+        if (st) *st = s;
+        guard.sh = nullptr;
+        *out = sh.release();
+    })
+}
+int fr_shard_levels(const fr_shard* sh, uint32_t* levels) {
+    FR_TRY({
+        NEED(sh && levels);
+        *levels = (uint32_t)sh->out_off.size();
+    })
+}
+int fr_shard_jobs(const fr_shard* sh, uint32_t level, uint32_t* jobs) {
+    FR_TRY({
+        NEED(sh && jobs && level < sh->out_off.size());
+        *jobs = (uint32_t)sh->out_off[level].size() - 1;
+    })
+}
+int fr_shard_outputs(const fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, uint32_t* n_lwe) {
+    FR_TRY({
+        NEED(sh && n_lwe);
+        uint32_t first, count;
+        shard_level_range(sh, level, begin, end, first, count);
+        *n_lwe = count;
+    })
+}
+int fr_shard_run(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end) {
+    FR_TRY({
+        NEED(ctx && sh);
+        uint32_t first, count;
+        shard_level_range(sh, level, begin, end, first, count);
+        const Plan& P = sh->plan;
+        const size_t a = P.level_off[level] + begin;
+        ctx->device().run_level_resident(P.d_gates + a, P.gates.data() + a, end - begin);
+    })
+}
+int fr_shard_export(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, uint64_t* dev_dst) {
+    FR_TRY({
+        NEED(ctx && sh);
+        uint32_t first, count;
+        const std::vector<int>& slots = shard_level_range(sh, level, begin, end, first, count);
+        NEED(dev_dst || !count);
+        ctx->device().slots_to_device(slots.data() + first, count, dev_dst);
+    })
+}
+int fr_shard_import(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, const uint64_t* dev_src) {
+    FR_TRY({
+        NEED(ctx && sh);
+        uint32_t first, count;
+        const std::vector<int>& slots = shard_level_range(sh, level, begin, end, first, count);
+        NEED(dev_src || !count);
+        ctx->device().device_to_slots(slots.data() + first, count, dev_src);
+    })
+}
+int fr_shard_finish(fr_ctx* ctx, fr_shard* sh, fr_ct* out, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && sh && out);
+        *out = finish_output(ctx, sh->out_gate, sh->out_w, sh->out_const, sh->plan.slot, false);
+        if (st) *st = sh->stats;
+    })
+}
+int fr_shard_free(fr_ctx* ctx, fr_shard* sh) {
+    FR_TRY({
+        NEED(ctx);
+        if (!sh) return FR_OK;
+        std::unique_ptr<fr_shard> own(sh);
+        if (ctx->dev) {
+            ctx->dev->sync();
+            free_plan_slots(*ctx->dev, sh->plan.slot);
+            ctx->dev->free_gates(sh->plan.d_gates);
+            sh->plan.d_gates = nullptr;
+        }
+    })
+}
+
+// The same schedule without a device (CPU evaluators, tests): every content
+// position of [0, n_chars) is taken as an encrypted radix character.
+int fr_schedule_match(size_t n_chars, const char* pattern, size_t lo, size_t hi, int32_t lowering, int32_t engine,
+                      int32_t grammar, int32_t multi_value, fr_job* jobs, size_t jobs_cap, size_t* n_jobs,
+                      uint32_t* level_off, size_t level_cap, size_t* n_levels, int32_t* out3) {
+    FR_TRY({
+        NEED(pattern && n_jobs && n_levels && out3 && lo <= hi);
+        ValueDag dag;
+        GrammarScope gs(grammar);
+        Recorded rec = record_has_match_engine(dag, n_chars, pattern, lo, hi, engine);
+        Program prog = lower(dag, rec.root, lowering);
+        Schedule S = build_schedule(prog.gates, n_chars, multi_value != 0, [](int cb, int& key, int&) {
+            key = cb;
+            return true;
+        });
+        *n_jobs = S.jobs.size();
+        *n_levels = S.level_off.size() - 1;
+        out3[0] = prog.out_gate;
+        out3[1] = prog.out_w;
+        out3[2] = prog.out_const;
+        if (jobs) {
+            NEED(jobs_cap >= S.jobs.size());
+            static_assert(sizeof(fr_job) == sizeof(DevGate), "fr_job mirrors DevGate");
+            std::memcpy(jobs, S.jobs.data(), sizeof(DevGate) * S.jobs.size());
+        }
+        if (level_off) {
+            NEED(level_cap >= S.level_off.size());
+            for (size_t l = 0; l < S.level_off.size(); ++l) level_off[l] = (uint32_t)S.level_off[l];
+        }
+    })
+}
+
+// device-to-device booleans (block 0 of a handle), e.g. per-rank partial results
+// gathered over RCCL: no host round trip of the LWE
+int fr_export_bool_device(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst) {
+    FR_TRY({
+        NEED(ctx && (h || !n) && (dev_dst || !n));
+        Device& dev = ctx->device();
+        std::vector<int> slots(n), tmp;
+        struct Guard {
+            Device& dev;
+            std::vector<int>& tmp;
+            ~Guard() {
+                for (int s : tmp) dev.free_slot(s);
+            }
+        } guard{dev, tmp};
+        for (size_t i = 0; i < n; ++i) {
+            const HandleRec& r = ctx->get(h[i]);
+            if (r.b[0].slot >= 0) {
+                slots[i] = r.b[0].slot;
+                continue;
+            }
+            // a trivial block 0 (e.g. a start range that cannot match): its trivial LWE
+            std::vector<uint64_t> lwe((size_t)ctx->p.lwe_len(), 0);
+            lwe.back() = (uint64_t)r.b[0].triv << DELTA_LOG;
+            tmp.push_back(dev.alloc_slot());
+            dev.write_slots(&tmp.back(), 1, lwe.data());
+            slots[i] = tmp.back();
+        }
+        dev.slots_to_device(slots.data(), n, dev_dst);
+    })
+}
+int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct* out) {
+    FR_TRY({
+        NEED(ctx && out && (dev_src || !n));
+        Device& dev = ctx->device();
+        std::vector<int> slots;
+        try {
+            for (size_t i = 0; i < n; ++i) slots.push_back(dev.alloc_slot());
+            dev.device_to_slots(slots.data(), n, dev_src);
+        } catch (...) {
+            for (int s : slots) dev.free_slot(s);
+            throw;
+        }
+        for (size_t i = 0; i < n; ++i) {
+            HandleRec r;
+            r.is_bool = true;
+            r.b[0].slot = slots[i];
+            out[i] = ctx->new_handle(r);
+        }
+    })
+}
+int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates) {
+    FR_TRY({
+        NEED(ctx);
+        Device& dev = ctx->device();
+        dev.sync();
+        const DeviceTimers& t = dev.timers();
+        if (br_ms) *br_ms = t.br_ms;
+        if (ks_ms) *ks_ms = t.ks_ms;
+        if (br_launches) *br_launches = t.br_launches;
+        if (br_gates) *br_gates = t.br_gates;
+    })
+}

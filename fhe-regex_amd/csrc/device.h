@@ -66,6 +66,10 @@ class Device {
     void free_slot(int s);
     void write_slots(const int* slots, size_t n, const uint64_t* host /* n * lwe_len */);
     void read_slot(int slot, uint64_t* host /* lwe_len */);
+    // packed device-to-device copies of slots (lwe_len u64 each) to / from a device
+    // buffer owned by the caller; both synchronise the library's stream on return
+    void slots_to_device(const int* slots, size_t n, uint64_t* dst);
+    void device_to_slots(const int* slots, size_t n, const uint64_t* src);
     void zero_slot(int slot);
 
     // run one dependency level of gates (all independent), async on the stream
@@ -114,6 +118,9 @@ class Device {
     void launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream);
     void free_fft();
     void build_ksk_limbs();  // d_kl_ from d_ksk_
+    void stage_slot_list(const int* slots, size_t n);  // -> d_slot_list_ (stream order)
+    int* d_slot_list_ = nullptr;
+    size_t slot_list_cap_ = 0;
 
     Params p_;
     int dev_;

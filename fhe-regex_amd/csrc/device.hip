@@ -1012,6 +1012,7 @@ Device::~Device() {
     (void)hipFree(d_arena_);
     (void)hipFree(d_gates_);
     (void)hipFree(d_ks_);
+    (void)hipFree(d_slot_list_);
     for (auto* h : h_stage_)
         if (h) (void)hipHostFree(h);
     for (auto* e : stage_ev_)
@@ -1087,6 +1088,48 @@ int Device::alloc_slot() {
 }
 void Device::free_slot(int s) {
     if (s >= 0) free_slots_.push_back(s);
+}
+
+// packed copies between arena slots and a device buffer of the caller (the
+// multi-rank exchange of a level's outputs: fr_shard_export / fr_shard_import):
+// one workgroup per LWE, lwe_len u64 each, coalesced
+__global__ void __launch_bounds__(256) k_slots_to_buf(const uint64_t* __restrict__ arena, int stride,
+                                                      const int* __restrict__ slots, int len, uint64_t* __restrict__ buf) {
+    const uint64_t* s = arena + (size_t)slots[blockIdx.x] * stride;
+    uint64_t* d = buf + (size_t)blockIdx.x * len;
+    for (int c = threadIdx.x; c < len; c += 256) d[c] = s[c];
+}
+__global__ void __launch_bounds__(256) k_buf_to_slots(const uint64_t* __restrict__ buf, int len,
+                                                      const int* __restrict__ slots, int stride, uint64_t* __restrict__ arena) {
+    const uint64_t* s = buf + (size_t)blockIdx.x * len;
+    uint64_t* d = arena + (size_t)slots[blockIdx.x] * stride;
+    for (int c = threadIdx.x; c < len; c += 256) d[c] = s[c];
+}
+void Device::stage_slot_list(const int* slots, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (slots[i] < 0 || (size_t)slots[i] >= next_slot_) throw Error(FR_ERR_INVALID, "slot list: slot out of range");
+    if (n > slot_list_cap_) {
+        HIP_CHECK(hipStreamSynchronize(STREAM));
+        (void)hipFree(d_slot_list_);
+        d_slot_list_ = nullptr;
+        slot_list_cap_ = std::max<size_t>(n, 1024);
+        HIP_CHECK(hipMalloc(&d_slot_list_, 4 * slot_list_cap_));
+    }
+    HIP_CHECK(hipMemcpyAsync(d_slot_list_, slots, 4 * n, hipMemcpyHostToDevice, STREAM));
+}
+void Device::slots_to_device(const int* slots, size_t n, uint64_t* dst) {
+    if (!n) return;
+    stage_slot_list(slots, n);
+    k_slots_to_buf<<<(unsigned)n, 256, 0, STREAM>>>(d_arena_, p_.slot_stride(), d_slot_list_, p_.lwe_len(), dst);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(STREAM));  // the caller's stream may read dst now
+}
+void Device::device_to_slots(const int* slots, size_t n, const uint64_t* src) {
+    if (!n) return;
+    stage_slot_list(slots, n);
+    k_buf_to_slots<<<(unsigned)n, 256, 0, STREAM>>>(src, p_.lwe_len(), d_slot_list_, p_.slot_stride(), d_arena_);
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipStreamSynchronize(STREAM));  // the caller may reuse src now
 }
 
 void Device::write_slots(const int* slots, size_t n, const uint64_t* host) {

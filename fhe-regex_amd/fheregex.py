@@ -89,6 +89,14 @@ class Gate(C.Structure):
                 ("out", C.c_uint32)]
 
 
+class FrJob(C.Structure):
+    """fr_job: one rotation job of a match schedule (fr_schedule_match)."""
+    _fields_ = [("n_in", C.c_int32), ("offset", C.c_int32), ("in_ref", C.c_int32 * 16), ("in_w", C.c_int32 * 16),
+                ("n_out", C.c_int32), ("kind", C.c_int32), ("out_gate", C.c_int32 * 8), ("lut", (C.c_uint8 * 16) * 8)]
+
+
+JOB_MULTI, JOB_DIRECT, JOB_SIGN = 0, 1, 2
+
 u64p = C.POINTER(C.c_uint64)
 _lib = None
 
@@ -151,6 +159,23 @@ _SIGS = {
                                    C.POINTER(C.c_double), C.POINTER(C.c_double)]),
     "fr_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "fr_debug_scalar": (C.c_uint64, [C.c_int32, C.c_uint64, C.c_uint64]),
+    "fr_export_bool_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p]),
+    "fr_import_bool_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32)]),
+    "fr_device_timers": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint64)]),
+    "fr_shard_plan": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t,
+                                C.POINTER(C.c_void_p), C.POINTER(MatchStats)]),
+    "fr_shard_levels": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    "fr_shard_jobs": (C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "fr_shard_outputs": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.POINTER(C.c_uint32)]),
+    "fr_shard_run": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]),
+    "fr_shard_export": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "fr_shard_import": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "fr_shard_finish": (C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
+    "fr_shard_free": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "fr_schedule_match": (C.c_int, [C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32, C.c_int32,
+                                    C.c_int32, C.POINTER(FrJob), C.c_size_t, C.POINTER(C.c_size_t),
+                                    C.POINTER(C.c_uint32), C.c_size_t, C.POINTER(C.c_size_t), C.POINTER(C.c_int32)]),
 }
 
 
@@ -412,6 +437,21 @@ class Context:
                                             C.byref(out), C.byref(st)))
         return out.value, st
 
+    def export_bool_device(self, hs: Sequence[int], dev_ptr: int):
+        arr = (C.c_uint32 * len(hs))(*hs)
+        _check(lib().fr_export_bool_device(self.h, arr, len(hs), C.c_void_p(dev_ptr)))
+
+    def import_bool_device(self, dev_ptr: int, n: int) -> List[int]:
+        out = (C.c_uint32 * n)()
+        _check(lib().fr_import_bool_device(self.h, C.c_void_p(dev_ptr), n, out))
+        return list(out)
+
+    def device_timers(self):
+        br, ks = C.c_double(), C.c_double()
+        nl, ng = C.c_uint64(), C.c_uint64()
+        _check(lib().fr_device_timers(self.h, C.byref(br), C.byref(ks), C.byref(nl), C.byref(ng)))
+        return {"br_ms": br.value, "ks_ms": ks.value, "br_launches": nl.value, "br_gates": ng.value}
+
     # single-stage device entry points
     def dev_keyswitch(self, lwes: np.ndarray) -> np.ndarray:
         a = np.ascontiguousarray(lwes.reshape(-1, self.lwe_len), dtype=np.uint64)
@@ -498,6 +538,144 @@ def shard_starts(L: int, world: int, rank: int) -> Tuple[int, int]:
     base, extra = divmod(L, world)
     lo = rank * base + min(rank, extra)
     return lo, lo + base + (1 if rank < extra else 0)
+
+
+# ------------------------------------------------------- one match across ranks
+def job_slice(J: int, world: int, rank: int) -> Tuple[int, int]:
+    """Contiguous slice [a, b) of a level's J rotation jobs owned by `rank`
+    (ceil(r J / world) boundaries: balanced, and rank 0 owns a lone job)."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    return -(-rank * J // world), -(-(rank + 1) * J // world)
+
+
+def run_sharded(ex, world: int, rank: int, all_gather):
+    """Level-sharded evaluation of one match plan (fheregex.h fr_shard_*):
+    every level but the last is split into contiguous job slices, each rank runs
+    its slice, and the slices' output LWEs are all-gathered so that every rank
+    holds the level; rank 0 runs the last level.  `ex` is an executor (ShardPlan
+    on the GPU, or a CPU evaluator in tests) with levels / jobs(l) /
+    outputs(l, a, b) / run(l, a, b) / export(l, a, b, cap) -> buffer /
+    import_(l, a, b, buffer); all_gather(buffer) returns every rank's buffer in
+    rank order.  Returns the number of gathered LWEs."""
+    gathered = 0
+    nl = ex.levels
+    for l in range(nl - 1):
+        parts = [job_slice(ex.jobs(l), world, r) for r in range(world)]
+        counts = [ex.outputs(l, a, b) for a, b in parts]
+        a, b = parts[rank]
+        if b > a:
+            ex.run(l, a, b)
+        bufs = all_gather(ex.export(l, a, b, max(counts)))
+        for r, (ar, br) in enumerate(parts):
+            if r != rank and counts[r]:
+                ex.import_(l, ar, br, bufs[r])
+        gathered += sum(counts)
+    if rank == 0 and nl:
+        ex.run(nl - 1, 0, ex.jobs(nl - 1))
+    return gathered
+
+
+class ShardPlan:
+    """fr_shard_* executor for run_sharded: a compiled, device-resident plan of one
+    match; buffers are torch CUDA tensors (export / import go device to device)."""
+
+    def __init__(self, ctx: Context, content: Sequence[int], pattern: str, start_lo: int = 0,
+                 start_hi: Optional[int] = None):
+        self.ctx = ctx
+        arr = (C.c_uint32 * len(content))(*content)
+        hi = len(content) if start_hi is None else start_hi
+        h = C.c_void_p()
+        self.stats = MatchStats()
+        _check(lib().fr_shard_plan(ctx.h, arr, len(content), pattern.encode("latin-1"), start_lo, hi, C.byref(h),
+                                   C.byref(self.stats)))
+        self.h = h
+        n = C.c_uint32()
+        _check(lib().fr_shard_levels(h, C.byref(n)))
+        self.levels = n.value
+        self._jobs = []
+        for l in range(self.levels):
+            _check(lib().fr_shard_jobs(h, l, C.byref(n)))
+            self._jobs.append(n.value)
+
+    def jobs(self, level: int) -> int:
+        return self._jobs[level]
+
+    def outputs(self, level: int, a: int, b: int) -> int:
+        n = C.c_uint32()
+        _check(lib().fr_shard_outputs(self.h, level, a, b, C.byref(n)))
+        return n.value
+
+    def run(self, level: int, a: int, b: int):
+        _check(lib().fr_shard_run(self.ctx.h, self.h, level, a, b))
+
+    def export(self, level: int, a: int, b: int, cap: int):
+        import torch
+        buf = torch.empty(max(cap, 1) * self.ctx.lwe_len, dtype=torch.int64, device=f"cuda:{self.ctx.device}")
+        _check(lib().fr_shard_export(self.ctx.h, self.h, level, a, b, C.c_void_p(buf.data_ptr())))
+        return buf
+
+    def import_(self, level: int, a: int, b: int, buf):
+        _check(lib().fr_shard_import(self.ctx.h, self.h, level, a, b, C.c_void_p(buf.data_ptr())))
+
+    def finish(self) -> Tuple[int, MatchStats]:
+        out = C.c_uint32()
+        st = MatchStats()
+        _check(lib().fr_shard_finish(self.ctx.h, self.h, C.byref(out), C.byref(st)))
+        return out.value, st
+
+    def free(self):
+        if getattr(self, "h", None):
+            _check(lib().fr_shard_free(self.ctx.h, self.h))
+            self.h = None
+
+
+def torch_all_gather(group=None):
+    """all_gather for run_sharded over torch.distributed (RCCL on GPU tensors):
+    the returned views of one gathered tensor are valid once this returns."""
+    import torch
+    import torch.distributed as dist
+
+    staged = dist.get_backend(group) == "gloo"  # gloo rehearsal: device buffers go through the host
+
+    def gather(buf):
+        world = dist.get_world_size(group)
+        src = buf.cpu() if staged and buf.is_cuda else buf
+        out = torch.empty(world * src.numel(), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(out, src, group=group)
+        if staged and buf.is_cuda:
+            out = out.to(buf.device)
+        if out.is_cuda:
+            torch.cuda.synchronize(out.device)  # the library reads it on its own stream
+        return list(out.view(world, -1))
+    return gather
+
+
+@dataclass
+class Schedule:
+    """fr_schedule_match: rotation jobs by level, without a device."""
+    jobs: list
+    level_off: List[int]
+    out_gate: int
+    out_w: int
+    out_const: int
+    n_gates: int
+
+
+def schedule_match(n_chars: int, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None,
+                   lowering: int = LOWER_THRESHOLD, engine: int = ENGINE_AUTO, grammar: int = GRAMMAR_REFERENCE,
+                   multi_value: bool = True) -> Schedule:
+    hi = n_chars if start_hi is None else start_hi
+    nj, nl = C.c_size_t(), C.c_size_t()
+    out3 = (C.c_int32 * 3)()
+    pat = pattern.encode("latin-1")
+    args = (n_chars, pat, start_lo, hi, lowering, engine, grammar, int(multi_value))
+    _check(lib().fr_schedule_match(*args, None, 0, C.byref(nj), None, 0, C.byref(nl), out3))
+    jobs = (FrJob * max(nj.value, 1))()
+    off = (C.c_uint32 * (nl.value + 1))()
+    _check(lib().fr_schedule_match(*args, jobs, len(jobs), C.byref(nj), off, len(off), C.byref(nl), out3))
+    n_gates = 1 + max([max(j.out_gate[f] for f in range(j.n_out)) for j in jobs[:nj.value]] or [-1])
+    return Schedule(list(jobs[:nj.value]), list(off), out3[0], out3[1], out3[2], n_gates)
 
 
 def header_symbols() -> List[str]:

@@ -118,9 +118,10 @@ int fr_set_keygen(fr_ctx* ctx, int32_t where);
 /* Export the server key: ksk = kN*ks_level*(n+1) u64 ; bsk = W*(k+1)^2*N u64
  * (coefficient domain, torus 2^64 (FFT ring) or mod Q = 998244353*1004535809
  * (RNS ring), layout [w][row][component][coef]).
- * k = 1: bootstrapping-key unrolling, W = 3*ceil(n/2) GGSWs, w = 3t+g encrypts
- * s_2t*s_2t+1, s_2t*(1-s_2t+1), (1-s_2t)*s_2t+1 for g = 0, 1, 2; k > 1: W = n,
- * GGSW w encrypts s_w.  Sizes from fr_server_key_sizes.  Either may be NULL. */
+ * k = 1 or the FFT ring: bootstrapping-key unrolling, W = 3*ceil(n/2) GGSWs,
+ * w = 3t+g encrypts s_2t*s_2t+1, s_2t*(1-s_2t+1), (1-s_2t)*s_2t+1 for g = 0, 1, 2;
+ * RNS ring with k > 1: W = n, GGSW w encrypts s_w.  Sizes from
+ * fr_server_key_sizes.  Either may be NULL. */
 int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
 int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len);
 
@@ -201,6 +202,65 @@ int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* 
 int fr_set_plan_cache(fr_ctx* ctx, size_t capacity);
 int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
                        size_t start_hi, fr_ct* out, fr_match_stats* stats);
+
+/* Booleans (block 0 of each handle) to / from a device buffer of n * (kN+1) u64
+ * (the start-offset shards' partial results gathered over RCCL without a host
+ * round trip; the reference's final ct_or fold, engine.rs:22-35).  Both
+ * synchronise the library's stream before returning. */
+int fr_export_bool_device(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst);
+int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct* out);
+/* Accumulated kernel timers of the profiling mode (fr_set_profiling): blind
+ * rotation and keyswitch milliseconds, launches and bootstraps. */
+int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates);
+
+/* ----- one match split across ranks ----- */
+/* The reference folds ct_or over the branches of every start offset
+ * (engine.rs:15-35, each branch a chain of execution.rs:76-190 calls); anchored
+ * patterns have one start (engine.rs:51-57), so start offsets alone do not
+ * spread their work.  A shard plan splits every dependency level of the lowered
+ * circuit instead: each rank compiles the same plan over its copy of the
+ * content (same pattern, content length and start range on every rank), runs a
+ * contiguous slice [begin, end) of each level's rotation jobs, exports the
+ * slice's output LWEs (kN+1 u64 each, job order) into a device buffer, and after
+ * an all-gather imports the other ranks' slices; the last level's output then
+ * exists on the ranks that hold it (fr_shard_finish).  Levels are 0-based.
+ * export / import synchronise the library's stream before returning; the
+ * caller orders its own stream (the all-gather) around them. */
+typedef struct fr_shard fr_shard;
+int fr_shard_plan(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
+                  size_t start_hi, fr_shard** out, fr_match_stats* stats);
+int fr_shard_levels(const fr_shard* sh, uint32_t* levels);
+int fr_shard_jobs(const fr_shard* sh, uint32_t level, uint32_t* jobs);
+int fr_shard_outputs(const fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, uint32_t* n_lwe);
+int fr_shard_run(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end); /* async */
+int fr_shard_export(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, uint64_t* dev_dst);
+int fr_shard_import(fr_ctx* ctx, fr_shard* sh, uint32_t level, uint32_t begin, uint32_t end, const uint64_t* dev_src);
+/* boolean result handle (valid on a rank that ran or imported the last level) */
+int fr_shard_finish(fr_ctx* ctx, fr_shard* sh, fr_ct* out, fr_match_stats* stats);
+int fr_shard_free(fr_ctx* ctx, fr_shard* sh);
+
+/* The schedule of such a plan without a device (CPU evaluators, tests): rotation
+ * job j of level l is jobs[level_off[l] .. level_off[l+1]); every content
+ * position of [0, n_chars) counts as an encrypted radix character.  in_ref[q] >= 0
+ * is the output of program gate in_ref[q], in_ref[q] < 0 content block
+ * -1 - in_ref[q] (= 4 pos + block, LSB block first); job input s = offset/2 +
+ * sum w_q in_q (units of Delta); kind 1: out_gate[0] = lut[0][s]; kind 0
+ * (multi-value): out_gate[f] = lut[f][s], f < n_out; kind 2: [s > 0].  out3 =
+ * (out_gate, out_w, out_const): result = out_const + out_w * gate (out_gate < 0:
+ * the constant).  Pass jobs / level_off = NULL to query the sizes. */
+typedef struct {
+    int32_t n_in;
+    int32_t offset;
+    int32_t in_ref[16];
+    int32_t in_w[16];
+    int32_t n_out;
+    int32_t kind;
+    int32_t out_gate[8];
+    uint8_t lut[8][16];
+} fr_job;
+int fr_schedule_match(size_t n_chars, const char* pattern, size_t start_lo, size_t start_hi, int32_t lowering,
+                      int32_t engine, int32_t grammar, int32_t multi_value, fr_job* jobs, size_t jobs_cap,
+                      size_t* n_jobs, uint32_t* level_off, size_t level_cap, size_t* n_levels, int32_t* out3);
 
 /* ----- host-only introspection (tests; no device needed) ----- */
 /* Canonical AST string of parse(pattern) (parser.rs:146-185). */

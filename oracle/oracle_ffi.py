@@ -273,6 +273,48 @@ class Oracle:
         lib().or_gates(self._pk, ptr(self.ksk), arr, len(gates), ptr(s), first, ptr(out))
         return out
 
+    def run_schedule(self, S, content_lwes: np.ndarray, levels=None) -> np.ndarray:
+        """Evaluate a match schedule (fheregex.schedule_match: fr_job semantics)
+        level by level, each level's jobs in one parallel or_gates call; returns
+        the result LWE (block 0 of the boolean).  levels: optional range of levels
+        (the caller then reads self.sched_val)."""
+        content = content_lwes.reshape(-1, self.big + 1)
+        if levels is None:
+            self.sched_val = {}
+            levels = range(len(S.level_off) - 1)
+        val = self.sched_val
+        for l in levels:
+            rows, index, jobs = [], {}, []
+            js = S.jobs[S.level_off[l]:S.level_off[l + 1]]
+            for j in js:
+                ins = []
+                for q in range(j.n_in):
+                    r = j.in_ref[q]
+                    if r not in index:
+                        index[r] = len(rows)
+                        rows.append(val[r] if r >= 0 else content[-1 - r])
+                    ins.append((index[r], j.in_w[q]))
+                jobs.append((ins, j.offset, [list(j.lut[f]) for f in range(j.n_out)], j.kind))
+            outs = self.gates(jobs, np.stack(rows))
+            k = 0
+            for j in js:
+                for f in range(j.n_out):
+                    val[j.out_gate[f]] = outs[k]
+                    k += 1
+        out = np.zeros(self.big + 1, dtype=np.uint64)
+        if S.out_gate >= 0:
+            out = (np.uint64(S.out_w & 0xFFFFFFFFFFFFFFFF) * val[S.out_gate]).astype(np.uint64)
+        out[-1] += np.uint64((S.out_const << 59) & 0xFFFFFFFFFFFFFFFF)
+        return out
+
+    @staticmethod
+    def set_threads(t: int):
+        lib().or_set_threads(t)
+
+    @staticmethod
+    def num_threads() -> int:
+        return lib().or_num_threads()
+
 
 def load_fixture_key(path: str | None = None) -> dict:
     if path is None:

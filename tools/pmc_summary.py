@@ -5,13 +5,20 @@ FETCH_SIZE correction (x2 for 16-B-per-lane streaming reads,
 MI355X_MICROARCH.md HBM section).  Launches are grouped by grid size; the
 per-match average over the blind-rotation launches of one has_match is what
 bench.py reports as roofline.traffic.
-Usage: python3 tools/pmc_summary.py PROFDIR OUT.json
+The compute side: VALU wave-instructions (SQ_INSTS_VALU) per active-CU clock,
+active CUs = min(bootstraps, 256), clocks = GRBM_GUI_ACTIVE / 8 (the sum over the
+8 XCDs; MI355X_MICROARCH.md "DVFS give-back"), summed over the match's launches.
+The kernel source hash lets bench.py flag a summary of an older kernel as stale.
+Usage: python3 tools/pmc_summary.py PROFDIR OUT.json [k]
 """
 import collections
 import csv
+import hashlib
 import json
 import os
 import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def load(d, name):
@@ -20,7 +27,9 @@ def load(d, name):
     out = collections.defaultdict(lambda: collections.defaultdict(list))
     for r in rows:
         k = r["Kernel_Name"].split("(")[0].replace("void ", "")
-        out[(k, int(r["Grid_Size"]))][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        key = (k, int(r["Grid_Size"]))
+        out[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        out[key]["_wg"] = [float(r["Workgroup_Size"])]
     return out
 
 
@@ -35,7 +44,8 @@ def main():
             continue
         f = fetch[key]["FETCH_SIZE"]
         w = write.get(key, {}).get("WRITE_SIZE", [0.0])
-        ent = {"kernel": k, "grid": grid, "calls": len(f),
+        wg = fetch[key]["_wg"][0]
+        ent = {"kernel": k, "grid": grid, "bootstraps": int(grid // wg), "calls": len(f),
                "fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
         ent["hbm_bytes"] = ent["fetch_bytes"] + ent["write_bytes"]
         s = sq.get(key, {})
@@ -58,11 +68,18 @@ def main():
     match = [e for e in launches if e is not sat]
     per_launch = sum(e["hbm_bytes"] * e["calls"] for e in match) / max(1, sum(e["calls"] for e in match))
     ring = "fft" if any("blind_rotate_fft" in e.get("kernel", "") for e in launches) else "rns"
-    res = {"hbm_bytes_per_launch": per_launch, "ring": ring, "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the /abc/ match, averaged per launch",
+    valu = sum(e.get("valu_insts") or 0 for e in match)
+    cu_clk = sum(min(e["bootstraps"], 256) * e.get("grbm_gui_active_per_xcd", 0) for e in match)
+    src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
+    res = {"hbm_bytes_per_launch": per_launch, "ring": ring, "k": int(sys.argv[3]) if len(sys.argv) > 3 else 1,
+           "valu_per_cu_clk": valu / cu_clk if valu and cu_clk else None,
+           "kernel_sha": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16],
+           "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the match, averaged per "
+                   "launch; valu_per_cu_clk = sum SQ_INSTS_VALU / sum min(bootstraps, 256) GRBM_GUI_ACTIVE/8",
            "launches": launches}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
-    print(json.dumps({"hbm_bytes_per_launch": per_launch}, indent=1))
+    print(json.dumps({k: res[k] for k in ("hbm_bytes_per_launch", "valu_per_cu_clk", "kernel_sha")}, indent=1))
 
 
 if __name__ == "__main__":
