@@ -355,22 +355,39 @@ constexpr int fbr_min_waves() {
     if (K == 1) return E == 4 ? 4 : 2;
     return E == 4 ? 3 : 2;  // k = 2: 2 x 6 waves (E = 4); E = 8: the one-slot-ahead loads need > 168 VGPRs
 }
+// Fourier-key loads: buffer loads with the key's resource in SGPRs, the uniform part
+// of the offset (step, GGSW, row, slot) in soffset and the lane's byte offset as the
+// only VGPR operand, so a load costs no VALU address arithmetic (gfx950 raw buffer
+// resource: word 3 = 0x00020000; the key is < 2 GiB)
+typedef unsigned int fr_v4u __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t bsk_rsrc(const double2* bsk) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)bsk, 0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ double2 bsk_load(__amdgpu_buffer_rsrc_t r, uint32_t lane_off, uint32_t uoff) {
+    const fr_v4u v = __builtin_amdgcn_raw_buffer_load_b128(r, (int)lane_off, (int)uoff, 0);
+    double2 d;
+    __builtin_memcpy(&d, &v, 16);
+    return d;
+}
+
 // row r != P of the MAC: the q-th other polynomial in ascending order
 template <int K>
 __device__ __forceinline__ int other_row(int P, int q) {
     return q < P ? q : q + 1;
 }
 // the 3 (K+1) Fourier GGSW values of slot m for this lane: [g][own row, other rows...]
-// (Fourier GGSW [r][c][m][lane]: row r, output column c = P)
+// (Fourier GGSW [r][c][m][lane]: row r, output column c = P; sbase: the step's byte offset)
 template <int M, int T, int K>
-__device__ __forceinline__ void load_slot(double2 (&B)[3][K + 1], const double2* bw, int P, int m, int tl) {
-    constexpr size_t GG = (size_t)(K + 1) * (K + 1) * M;
+__device__ __forceinline__ void load_slot(double2 (&B)[3][K + 1], __amdgpu_buffer_rsrc_t rs, uint32_t sbase, int P,
+                                          int m, uint32_t lane_off) {
+    constexpr uint32_t GG = (uint32_t)(K + 1) * (K + 1) * M;
 #pragma unroll
     for (int gg = 0; gg < 3; ++gg) {
-        B[gg][0] = (bw + (size_t)gg * GG + (size_t)(P * (K + 1) + P) * M + (size_t)m * T)[tl];
+        B[gg][0] = bsk_load(rs, lane_off, sbase + 16u * (gg * GG + (uint32_t)(P * (K + 1) + P) * M + (uint32_t)m * T));
 #pragma unroll
         for (int q = 0; q < K; ++q)
-            B[gg][1 + q] = (bw + (size_t)gg * GG + (size_t)(other_row<K>(P, q) * (K + 1) + P) * M + (size_t)m * T)[tl];
+            B[gg][1 + q] = bsk_load(
+                rs, lane_off, sbase + 16u * (gg * GG + (uint32_t)(other_row<K>(P, q) * (K + 1) + P) * M + (uint32_t)m * T));
     }
 }
 
@@ -470,7 +487,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const double2* orow_bl[K];  // the other polynomials' rows, ascending
 #pragma unroll
     for (int q = 0; q < K; ++q) orow_bl[q] = xbuf + other_row<K>(P, q) * G::NP + G::template at<XL>(bl);
-    constexpr size_t GG = (size_t)(K + 1) * (K + 1) * M;  // complex values per Fourier GGSW: [r][c][m][lane]
+    constexpr uint32_t GG = (uint32_t)(K + 1) * (K + 1) * M;  // complex values per Fourier GGSW: [r][c][m][lane]
+    const __amdgpu_buffer_rsrc_t rs = bsk_rsrc(bsk);
+    const uint32_t lane_off = 16u * (uint32_t)tl;
     const int steps = (n + 1) / 2;
     // latency shape: Fourier GGSW slots of a step for this lane, [g][own, other rows][m],
     // and (k = 1) the lane's twiddles
@@ -485,8 +504,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     for (int t = 0; t < steps; ++t) {
         if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
         FBR_STAMP(0);
-        // (uniform base pointers in SGPRs + the lane offset: no per-load address VGPRs)
-        const double2* bw = bsk + (size_t)(3 * __builtin_amdgcn_readfirstlane(t)) * GG;
+        // the step's byte offset in the key (uniform: soffset of every load)
+        const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
         // latency shape: GGSW g's slots for this lane, issued in three groups spread
         // over the forward FFT (one group per phase boundary) so that no wave stalls on
         // a full load queue at the top of the step; they land before the MAC
@@ -497,11 +516,13 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
                 for (int r = 0; r <= K; ++r) gv[gg][r][m] = make_double2(t + gg + r, m);
 #else
-                gv[gg][0][m] = (bw + (size_t)gg * GG + (size_t)(P * (K + 1) + P) * M + (size_t)m * T)[tl];
+                gv[gg][0][m] = bsk_load(rs, lane_off,
+                                        sbase + 16u * (gg * GG + (uint32_t)(P * (K + 1) + P) * M + (uint32_t)m * T));
 #pragma unroll
                 for (int q = 0; q < K; ++q)
-                    gv[gg][1 + q][m] =
-                        (bw + (size_t)gg * GG + (size_t)(other_row<K>(P, q) * (K + 1) + P) * M + (size_t)m * T)[tl];
+                    gv[gg][1 + q][m] = bsk_load(
+                        rs, lane_off,
+                        sbase + 16u * (gg * GG + (uint32_t)(other_row<K>(P, q) * (K + 1) + P) * M + (uint32_t)m * T));
 #endif
             }
         };
@@ -566,7 +587,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         constexpr bool PRE0 = !LAT;  // slot 0 lands during the MAC barrier and row exchange
 #endif
         double2 Bc[3][K + 1];
-        if constexpr (PRE0) load_slot<M, T, K>(Bc, bw, P, 0, tl);
+        if constexpr (PRE0) load_slot<M, T, K>(Bc, rs, sbase, P, 0, lane_off);
         __syncthreads();
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
         // Slot m of this lane has L = Lb + M s_m: Lb = L mod M is shared by the
@@ -580,10 +601,10 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int m = 0; m < E; ++m) {
             double2 Bn[3][K + 1];
             if constexpr (AHEAD) {
-                if (m + 1 < E) load_slot<M, T, K>(Bn, bw, P, m + 1, tl);
+                if (m + 1 < E) load_slot<M, T, K>(Bn, rs, sbase, P, m + 1, lane_off);
                 __builtin_amdgcn_sched_barrier(0);
             } else if constexpr (!LAT) {
-                if (!PRE0 || m > 0) load_slot<M, T, K>(Bc, bw, P, m, tl);
+                if (!PRE0 || m > 0) load_slot<M, T, K>(Bc, rs, sbase, P, m, lane_off);
             }
             const double2 own = x[m];
             double2 oth[K];
