@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 out=${1:-gpurun_out/check}
 mkdir -p "$out"
 export TMPDIR=/tmp
-step() { local t=$1; shift; echo "== $*"; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
+step() { local t=$1; shift; echo "== $*" >&2; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
 if [ "$2" != "skip-tests" ]; then
   step 400 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -40 "$out/gpu_tests.log"; exit 1; }
   tail -3 "$out/gpu_tests.log"

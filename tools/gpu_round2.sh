@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 out=${1:-gpurun_out/r2}
 mkdir -p "$out"
 export TMPDIR=/tmp
-step() { local t=$1; shift; echo "== $*"; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
+step() { local t=$1; shift; echo "== $*" >&2; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
 step 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -40 "$out/gpu_tests.log"; exit 1; }
 tail -2 "$out/gpu_tests.log"
 step 200 python __graft_entry__.py smoke > "$out/smoke.log" 2>&1 || { cat "$out/smoke.log"; exit 1; }

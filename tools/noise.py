@@ -5,10 +5,13 @@ phase - expected*Delta on the 2^64 torus (signed), reported as log2 of the
 standard deviation and of the max |error|:
   fresh    : fresh encryptions (glwe sigma)
   ks       : after keyswitch to the small key (2048 -> 742)
+  ms       : after the modulus switch of the keyswitched LWE to 2N (the phase the blind
+             rotation decides on; in torus units, decision threshold Delta/2 = 2^58),
+             with the Gaussian failure estimate per bootstrap erfc(2^58 / (sqrt 2 sigma))
   direct   : blind rotation of the LUT polynomial (identity LUT)
   multi    : multi-value outputs (w-step), per LUT norm^2
   sign     : sign-gate outputs
-Usage: python3 tools/noise.py [count] [out.json]
+Usage: [FR_PARAMS=k2n1024] python3 tools/noise.py [count] [out.json]
 """
 import json
 import math
@@ -52,7 +55,8 @@ def main():
     with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
         blob = f.read()
     ring = {"fft": F.RING_FFT, "rns": F.RING_RNS}.get(os.environ.get("FR_RING", ""))
-    ctx = F.Context(0, params=F.default_params(ring=ring))
+    k, N = (2, 1024) if os.environ.get("FR_PARAMS") == "k2n1024" else (1, 2048)
+    ctx = F.Context(0, params=F.default_params(k=k, N=N, ring=ring))
     ctx.load_client_key(blob)
     ctx.gen_server_key(42)
     rng = np.random.default_rng(1)
@@ -63,6 +67,16 @@ def main():
         res["fresh"] = stats(signed(phase(fresh, s_big) - msgs.astype(np.uint64) * np.uint64(DELTA)))
         ks = ctx.dev_keyswitch(fresh)
         res["ks"] = stats(signed(phase(ks, s_small) - msgs.astype(np.uint64) * np.uint64(DELTA)))
+        # modulus switch to 2N: round(x 2N / 2^64) per coefficient, phase in Z_2N
+        l2 = int(math.log2(2 * N))
+        ab = ((ks >> np.uint64(64 - l2 - 1)) + np.uint64(1)) >> np.uint64(1)
+        ab &= np.uint64(2 * N - 1)
+        ph = (ab[:, -1].astype(np.int64) - (ab[:, :-1].astype(np.int64) * s_small.astype(np.int64)).sum(axis=1)) % (2 * N)
+        err = (ph - msgs.astype(np.int64) * (2 * N // 32)) % (2 * N)
+        err = np.where(err >= N, err - 2 * N, err).astype(np.float64) * 2.0 ** (64 - l2)
+        res["ms"] = stats(err)
+        sd = float(np.std(err))
+        res["ms"]["fail_per_bootstrap"] = math.erfc(2.0 ** 58 / (math.sqrt(2) * sd)) if sd > 0 else 0.0
         ident = [list(range(16))] * count
         out = ctx.dev_blind_rotate(ks, ident)
         res["direct"] = stats(signed(phase(out, s_big) - msgs.astype(np.uint64) * np.uint64(DELTA)))
@@ -88,6 +102,7 @@ def main():
         res["sign"] = stats(np.array(errs))
     res["threshold_log2"] = 58.0
     res["ring"] = "fft" if ctx.params.ring == F.RING_FFT else "rns"
+    res["params"] = f"k{k}n{N}"
     print(json.dumps(res, indent=1))
     if out_path:
         with open(out_path, "w") as f:
