@@ -395,3 +395,35 @@ def test_k2_n1024_params_rns(key_blob, fixture_key):
     assert (got[0] == O.blind_rotate(ks[0], lut)).all()
     got, st = _config(ctx, "xxabcx", "/abc/", 11)
     assert got == 1
+
+
+def test_fuzz_encrypted_vs_oracle(gctx):
+    """Seeded random patterns (the reference grammar, tests/regex_fuzz.py) on random
+    encrypted content of 1-10 chars (engine AUTO), each decrypted result against the
+    oracle's position-set simulator (polynomial; the enumerating oracle's counters are
+    checked on the host, tests/test_host.py), the reference's Err / panic reproduced;
+    the plan cache evicts as it goes."""
+    import random
+
+    import regex_fuzz as rf
+    rng = random.Random(11)
+    n = errs = 0
+    while n < 60:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(1, 10))
+        try:
+            exp = ro.has_match_reach(c, p)
+        except (ro.ParseError, ro.ReferencePanic) as e:
+            hs = gctx.encrypt_upload_str(c, seed=n)
+            with pytest.raises(F.ParseError if isinstance(e, ro.ParseError) else F.ReferencePanic):
+                gctx.has_match(hs, p)
+            for h in hs:
+                gctx.release(h)
+            errs += 1
+            continue
+        hs = gctx.encrypt_upload_str(c, seed=n)
+        out, st = gctx.has_match(hs, p)
+        assert gctx.decrypt_radix(gctx.download_radix(out)) == exp, (c, p)
+        for h in hs + [out]:
+            gctx.release(h)
+        n += 1
