@@ -101,6 +101,15 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_LAT_LOAD2
 #define FR_LAT_LOAD2 3
 #endif
+// latency shape: how many of a step's three GGSW groups are loaded right after the
+// previous step's MAC (the rest across the step's own forward FFT)
+#ifndef FR_LAT_PF
+#define FR_LAT_PF 2
+#endif
+// latency shape, k = 1: the lane's twiddles in registers (1) or read from LDS (0)
+#ifndef FR_LAT_TWR
+#define FR_LAT_TWR 1
+#endif
 
 template <int M, int E>
 struct FTwr {
@@ -245,6 +254,9 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl)
         static_assert(!PRE, "register exchanges replace only exchanges without a pre-barrier");
         fperm_exchange<M, E, PF, PT>(x);
     } else {
+#ifdef FR_FFT_NOXCHG  // timing experiment only (wrong results): LDS exchanges skipped
+        return;
+#endif
         constexpr int X = PF < PT ? PF : PT;
         double2* rf = row + G::template at<X>(G::template base<PF>(tl));
         double2* rt = row + G::template at<X>(G::template base<PT>(tl));
@@ -341,7 +353,7 @@ template <int N, int K, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
     return 16 * ((LAT ? 2 : 1) * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 +
                  (LAT ? (size_t)N : (size_t)N / 2)) +
-           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT;
+           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT + 2 * 514;
 }
 // workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
 template <int K, int E>
@@ -428,7 +440,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     static_assert(!LAT || E == 4, "the latency shape holds a step's GGSW values in registers: E = 4");
     constexpr int T = M / E, NT = (K + 1) * T, LAST = G::NPH - 1, XL = G::XL;
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
-    constexpr bool TWR = LAT && K == 1;  // twiddles in registers
+    constexpr bool TWR = LAT && K == 1 && FR_LAT_TWR;  // twiddles in registers
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
     double2* xbuf = fsm;                  // K+1 rows of NP complex: row P at P * NP
     double2* ibuf = LAT ? xbuf + (K + 1) * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
@@ -439,6 +451,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
     uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
     int* wcnt = (int*)(wterms + 16 * MAX_OUT);
+    uint16_t* nxt = (uint16_t*)(wcnt + MAX_OUT);  // (latency shape) next unskipped step >= t, t <= steps
 
     const int tid = threadIdx.x;
     const int P = __builtin_amdgcn_readfirstlane(tid / T), tl = tid % T;  // wave-uniform polynomial
@@ -501,32 +514,49 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     uint64_t tlast = __builtin_amdgcn_s_memtime();
     const uint64_t tstart = tlast;
 #endif
+    // latency shape: GGSW g's slots of step tt for this lane ([g][own, other rows][m])
+    auto load_ggsw = [&](int gg, int tt) {
+        const uint32_t sb = (uint32_t)__builtin_amdgcn_readfirstlane(tt) * (3u * GG * 16u);
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+#ifdef FR_FFT_NOBSK  // timing experiment only (wrong results): no GGSW traffic
+#pragma unroll
+            for (int r = 0; r <= K; ++r) gv[gg][r][m] = make_double2(tt + gg + r, m);
+#else
+            gv[gg][0][m] =
+                bsk_load(rs, lane_off, sb + 16u * (gg * GG + (uint32_t)(P * (K + 1) + P) * M + (uint32_t)m * T));
+#pragma unroll
+            for (int q = 0; q < K; ++q)
+                gv[gg][1 + q][m] = bsk_load(
+                    rs, lane_off,
+                    sb + 16u * (gg * GG + (uint32_t)(other_row<K>(P, q) * (K + 1) + P) * M + (uint32_t)m * T));
+#endif
+        }
+    };
+    // latency shape, LATPF: groups 0 .. NPF-1 of a step's key values are loaded one
+    // step ahead -- right after the previous step's MAC, when their registers are dead --
+    // so that they have the inverse FFT, the accumulate and the forward FFT to land (a
+    // single CU streams ~50 GB/s of key at 3.9 us per step); the others across the
+    // step's own forward FFT.  The next unskipped step comes from the table nxt (no
+    // control flow around the prefetch, which keeps it after the MAC's last use).
+    constexpr int NPF = LAT && K == 1 ? FR_LAT_PF : 0;  // (k = 2: no VGPR room)
+    constexpr bool LATPF = NPF > 0;
+    if constexpr (LATPF) {
+        for (int t = tid; t <= steps; t += NT) {
+            int tt = t;
+            while (tt < steps && (abar[2 * tt] | abar[2 * tt + 1]) == 0) ++tt;
+            nxt[t] = (uint16_t)tt;
+        }
+        __syncthreads();
+        const int t0 = __builtin_amdgcn_readfirstlane((int)nxt[0]);
+        for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, t0 < steps ? t0 : 0);
+    }
     for (int t = 0; t < steps; ++t) {
         if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
         FBR_STAMP(0);
         // the step's byte offset in the key (uniform: soffset of every load)
         const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
-        // latency shape: GGSW g's slots for this lane, issued in three groups spread
-        // over the forward FFT (one group per phase boundary) so that no wave stalls on
-        // a full load queue at the top of the step; they land before the MAC
-        auto load_ggsw = [&](int gg) {
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-#ifdef FR_FFT_NOBSK  // timing experiment only (wrong results): no GGSW traffic
-#pragma unroll
-                for (int r = 0; r <= K; ++r) gv[gg][r][m] = make_double2(t + gg + r, m);
-#else
-                gv[gg][0][m] = bsk_load(rs, lane_off,
-                                        sbase + 16u * (gg * GG + (uint32_t)(P * (K + 1) + P) * M + (uint32_t)m * T));
-#pragma unroll
-                for (int q = 0; q < K; ++q)
-                    gv[gg][1 + q][m] = bsk_load(
-                        rs, lane_off,
-                        sbase + 16u * (gg * GG + (uint32_t)(other_row<K>(P, q) * (K + 1) + P) * M + (uint32_t)m * T));
-#endif
-            }
-        };
-        if constexpr (LAT) load_ggsw(0);
+        if constexpr (LAT && NPF < 1) load_ggsw(0, t);
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
         const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
         constexpr int NB = E / 4;
@@ -562,22 +592,24 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
             if constexpr (LAT) {
                 constexpr int p = decltype(ph)::value;
-                if constexpr (p == FR_LAT_LOAD1) {
+                if constexpr (p == FR_LAT_LOAD1 && NPF < 2) {
                     __builtin_amdgcn_sched_barrier(0);
-                    load_ggsw(1);
+                    load_ggsw(1, t);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if constexpr (p == FR_LAT_LOAD2) {
+                if constexpr (p == FR_LAT_LOAD2 && NPF < 3) {
                     __builtin_amdgcn_sched_barrier(0);
-                    load_ggsw(2);
+                    load_ggsw(2, t);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
         });
         FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
+#ifndef FR_FFT_NOMACX  // timing experiment only (wrong results): no MAC exchange
 #pragma unroll
         for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
+#endif
         // throughput shapes: slot m's GGSW values, loaded one slot ahead (E = 8) or
         // at the top of the slot (E = 4, 128 VGPRs: the other workgroup hides the wait)
         constexpr bool AHEAD = !LAT && E == 8;
@@ -588,7 +620,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #endif
         double2 Bc[3][K + 1];
         if constexpr (PRE0) load_slot<M, T, K>(Bc, rs, sbase, P, 0, lane_off);
+#ifndef FR_FFT_NOMACX
         __syncthreads();
+#endif
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
         // Slot m of this lane has L = Lb + M s_m: Lb = L mod M is shared by the
         // slots of equal m >> 2 (E/4 bases per lane) and s_m = brv2(m & 3) (fft.h: L(j) =
@@ -609,7 +643,11 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             const double2 own = x[m];
             double2 oth[K];
 #pragma unroll
+#ifdef FR_FFT_NOMACX
+            for (int q = 0; q < K; ++q) oth[q] = make_double2(own.y, own.x);
+#else
             for (int q = 0; q < K; ++q) oth[q] = orow_bl[q][G::template at<XL>(G::template moff<LAST>(m))];
+#endif
             const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
             double cr[3], ci[3];
 #pragma unroll
@@ -644,6 +682,12 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
                     for (int r = 0; r <= K; ++r) Bc[gg][r] = Bn[gg][r];
             }
+        }
+        if constexpr (LATPF) {  // the next step's key, into the registers the MAC just freed
+            const int tn = __builtin_amdgcn_readfirstlane((int)nxt[t + 1]);
+            __builtin_amdgcn_sched_barrier(0);
+            for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, tn < steps ? tn : t);
+            __builtin_amdgcn_sched_barrier(0);
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
