@@ -50,7 +50,7 @@ class Device {
 
     // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod Q [i][r][c][coef]
     void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
-    bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk_); }
+    bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk4_); }
     // server-key generation on the device (keygen.hip; FFT ring): the same keys
     // as gen_ksk + gen_bsk on the host, bit for bit; the torus keys stay on the
     // device for download_server_key
@@ -144,7 +144,7 @@ class Device {
     // psi quadrant table, leaf exponents (fft.h)
     int fft_e_ = 4;           // complex points per lane in the throughput shape (4 or 8; 4 measured faster)
     size_t fft_small_ = 256;  // launches of at most this many bootstraps use the latency shape
-    double* d_fbsk_ = nullptr;  // layout for E = 8
+    double* d_fbsk_ = nullptr;  // layout for E = 8 (k = 2 only)
     double* d_fbsk4_ = nullptr;  // layout for E = 4
     double* d_ftw_ = nullptr;
     double* d_fqt_ = nullptr;   // psi^k, k < 2N

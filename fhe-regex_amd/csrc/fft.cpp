@@ -40,6 +40,13 @@ Tables::Tables(int n) : N(n), M(n / 2) {
         E.swap(next);
     }
     for (int j = 0; j < M; ++j) leaf[j] = (uint16_t)E[j];
+    // the radix-4 forms (fft_br.hip, inv_r4) take a stage's odd sibling as i times the
+    // even one: psi^(x + N/2) = i psi^x is an exact quarter turn of psi_pow
+    for (int s = 1; s < LOG; ++s)
+        for (int b = 0; b < (1 << (s - 1)); ++b) {
+            const c64 u = tw[(1 << s) + 2 * b], v = tw[(1 << s) + 2 * b + 1];
+            if (v.re != -u.im || v.im != u.re) throw Error(FR_ERR_INVALID, "fft: sibling twiddles are not i apart");
+        }
 }
 
 void Tables::forward(c64* z) const {
@@ -53,6 +60,20 @@ void Tables::forward(c64* z) const {
 }
 
 void Tables::inverse(c64* z) const {
+    if (LOG % 2 == 0) {  // stages (2p + 1, 2p) as radix-4 groups (inv_r4)
+        for (int s0 = LOG - 2; s0 >= 0; s0 -= 2) {
+            const int s1 = s0 + 1, h1 = M >> (s1 + 1), h0 = 2 * h1;
+            for (int b = 0; b < (1 << s0); ++b) {
+                const c64 c = tw[(1 << s0) + b], ca = tw[(1 << s1) + 2 * b];
+                c64 cc;
+                cmul(c.re, c.im, ca.re, ca.im, cc.re, cc.im);
+                for (int j = b * 2 * h0; j < b * 2 * h0 + h1; ++j)
+                    inv_r4(z[j].re, z[j].im, z[j + h1].re, z[j + h1].im, z[j + h0].re, z[j + h0].im, z[j + h0 + h1].re,
+                           z[j + h0 + h1].im, c.re, c.im, ca.re, ca.im, cc.re, cc.im);
+            }
+        }
+        return;
+    }
     for (int s = LOG - 1; s >= 0; --s) {
         const int h = M >> (s + 1);
         for (int b = 0; b < (1 << s); ++b) {

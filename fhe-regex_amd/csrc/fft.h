@@ -73,6 +73,28 @@ FR_HD void inv_bf(double& ur, double& ui, double& vr, double& vi, double cr, dou
     vr = FR_FMA(cr, dr, pr);
     vi = FR_FMA(cr, di, pi);
 }
+// inverse radix-4 group: stages s1 = 2p + 1 then s0 = 2p of an even-log2(M) inverse
+// transform on x0..x3 (x1 = x0's stage-s1 partner, x2 = its stage-s0 partner).  Stage
+// s1's twiddles are ca and i ca (siblings of the split tree, fft::Tables), stage s0's c:
+//   a = x0 + x1, d1 = x0 - x1, b = x2 + x3, d2 = x2 - x3,
+//   t1 = d1 - i d2, t2 = d1 + i d2                      (exact swaps and signs)
+//   x0 <- a + b, x1 <- conj(ca) t1, x2 <- conj(c) (a - b), x3 <- conj(cc) t2
+// with cc = c ca (cmul) and conj(w) d as in inv_bf: 28 operations for 4 x inv_bf's 32
+FR_HD void inv_r4(double& x0r, double& x0i, double& x1r, double& x1i, double& x2r, double& x2i, double& x3r,
+                  double& x3i, double cr, double ci, double car, double cai, double ccr, double cci) {
+    const double ar = x0r + x1r, ai = x0i + x1i, d1r = x0r - x1r, d1i = x0i - x1i;
+    const double br = x2r + x3r, bi = x2i + x3i, d2r = x2r - x3r, d2i = x2i - x3i;
+    const double t1r = d1r + d2i, t1i = d1i - d2r, t2r = d1r - d2i, t2i = d1i + d2r;
+    const double er = ar - br, ei = ai - bi;
+    x0r = ar + br;
+    x0i = ai + bi;
+    x1r = FR_FMA(car, t1r, cai * t1i);
+    x1i = FR_FMA(car, t1i, -(cai * t1r));
+    x2r = FR_FMA(cr, er, ci * ei);
+    x2i = FR_FMA(cr, ei, -(ci * er));
+    x3r = FR_FMA(ccr, t2r, cci * t2i);
+    x3i = FR_FMA(ccr, t2i, -(cci * t2r));
+}
 // psi^k (k in [0, 2N)) from the quadrant table qt[r] = psi^r, r < N/2:
 // psi^k = i^(k / (N/2)) psi^(k mod N/2); i * (a + bi) = -b + ai.
 FR_HD void psi_quadrant(double ar, double ai, uint32_t q, double& zr, double& zi) {
@@ -138,7 +160,7 @@ struct Tables {
     std::vector<uint16_t> leaf;  // [M]: L(j) = E(LOG, j) mod 2N
     explicit Tables(int N);
     void forward(c64* z) const;   // natural order -> slot order (M points)
-    void inverse(c64* z) const;   // slot order -> natural order, times M
+    void inverse(c64* z) const;   // slot order -> natural order, times M (radix-4 pairs, LOG even)
 };
 
 // Fourier bootstrapping key: every GGSW polynomial of the torus BSK

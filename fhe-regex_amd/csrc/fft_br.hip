@@ -60,6 +60,34 @@ constexpr int FV = fft_layout_variant(ilog2c(M), ilog2c(E));
 __device__ __forceinline__ void cfwd(double2& x, double2& y, double2 c) { fft::fwd_bf(x.x, x.y, y.x, y.y, c.x, c.y); }
 __device__ __forceinline__ void cinv(double2& u, double2& v, double2 c) { fft::inv_bf(u.x, u.y, v.x, v.y, c.x, c.y); }
 
+// k = 1 (log2 M even, E = 4): every phase is two stages s0 = 2p, s1 = 2p + 1 and the
+// inverse takes them as one radix-4 group (fft.h inv_r4).  A lane's twiddles of such a
+// phase are c (stage s0, both pairs), ca (stage s1, pair 0/1; pair 2/3 has i ca exactly,
+// fft::Tables) and cc = c ca (inverse only).
+template <int M, int E>
+constexpr bool fradix4() {
+    return E == 4 && FGeo<M, E>::LOG % 2 == 0;
+}
+template <int M, int E>
+struct FTwr {
+    static constexpr int COUNT = fradix4<M, E>() ? FGeo<M, E>::NPH * 3 : FGeo<M, E>::LOG * (E / 2);
+    double2 v[COUNT];
+};
+// i c (exact: a swap and a sign)
+__device__ __forceinline__ double2 fmul_i(double2 c) { return make_double2(-c.y, c.x); }
+__device__ __forceinline__ void cinv_r4(double2 (&x)[4], double2 c, double2 ca, double2 cc) {
+    fft::inv_r4(x[0].x, x[0].y, x[1].x, x[1].y, x[2].x, x[2].y, x[3].x, x[3].y, c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+}
+// the radix-4 twiddles (c, ca) of phase p for this lane from the LDS table
+template <int M, int E, int p>
+__device__ __forceinline__ void ftw_r4(const double2* tw, int tl, double2& c, double2& ca) {
+    using G = FGeo<M, E>;
+    constexpr int s0 = G::s_begin(p), s1 = s0 + 1;
+    const int b = G::template base<p>(tl);
+    c = (tw + (b >> (G::LOG - s0)))[(1 << s0) + (G::template moff<p>(0) >> (G::LOG - s0))];
+    ca = (tw + (b >> (G::LOG - s1)))[(1 << s1) + (G::template moff<p>(0) >> (G::LOG - s1))];
+}
+
 template <int M, int E, int p>
 __device__ __forceinline__ void ffwd_phase(double2 (&x)[E], const double2* tw, int tl) {
     using G = FGeo<M, E>;
@@ -73,6 +101,19 @@ __device__ __forceinline__ void ffwd_phase(double2 (&x)[E], const double2* tw, i
             if (m & dm) continue;
             cfwd(x[m], x[m + dm], zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))]);
         }
+    }
+}
+template <int M, int E, int p>
+__device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, int tl);
+template <int M, int E, int p>
+__device__ __forceinline__ void finv_phase_lds(double2 (&x)[E], const double2* tw, int tl) {
+    if constexpr (fradix4<M, E>()) {
+        double2 c, ca, cc;
+        ftw_r4<M, E, p>(tw, tl, c, ca);
+        fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+        cinv_r4(x, c, ca, cc);
+    } else {
+        finv_phase<M, E, p>(x, tw, tl);
     }
 }
 template <int M, int E, int p>
@@ -112,11 +153,6 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #endif
 
 template <int M, int E>
-struct FTwr {
-    static constexpr int COUNT = FGeo<M, E>::LOG * (E / 2);
-    double2 v[COUNT];
-};
-template <int M, int E>
 constexpr int ftw_index(int s, int m) {
     const int d = FGeo<M, E>::LOG - 1 - s - FGeo<M, E>::lo(s / FGeo<M, E>::e);
     return s * (E / 2) + ((m >> (d + 1)) << d) + (m & ((1 << d) - 1));
@@ -124,6 +160,14 @@ constexpr int ftw_index(int s, int m) {
 template <int M, int E, int p>
 __device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* tw, int tl) {
     using G = FGeo<M, E>;
+    if constexpr (fradix4<M, E>()) {
+        double2 c, ca, cc;
+        ftw_r4<M, E, p>(tw, tl, c, ca);
+        fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+        twr.v[3 * p] = c, twr.v[3 * p + 1] = ca, twr.v[3 * p + 2] = cc;
+        if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1>(twr, tw, tl);
+        return;
+    }
     const int b = G::template base<p>(tl);
 #pragma unroll
     for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
@@ -140,6 +184,14 @@ __device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* t
 template <int M, int E, int p>
 __device__ __forceinline__ void ffwd_phase_r(double2 (&x)[E], const FTwr<M, E>& twr) {
     using G = FGeo<M, E>;
+    if constexpr (fradix4<M, E>()) {  // stage s0: pairs (0, 2), (1, 3); stage s1: (0, 1), (2, 3)
+        const double2 c = twr.v[3 * p], ca = twr.v[3 * p + 1];
+        cfwd(x[0], x[2], c);
+        cfwd(x[1], x[3], c);
+        cfwd(x[0], x[1], ca);
+        cfwd(x[2], x[3], fmul_i(ca));
+        return;
+    }
 #pragma unroll
     for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
         const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
@@ -153,6 +205,10 @@ __device__ __forceinline__ void ffwd_phase_r(double2 (&x)[E], const FTwr<M, E>& 
 template <int M, int E, int p>
 __device__ __forceinline__ void finv_phase_r(double2 (&x)[E], const FTwr<M, E>& twr) {
     using G = FGeo<M, E>;
+    if constexpr (fradix4<M, E>()) {
+        cinv_r4(x, twr.v[3 * p], twr.v[3 * p + 1], twr.v[3 * p + 2]);
+        return;
+    }
 #pragma unroll
     for (int s = G::s_end(p) - 1; s >= G::s_begin(p); --s) {
         const int dm = 1 << (G::LOG - 1 - s - G::lo(p));
@@ -315,7 +371,7 @@ template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false>
 __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, int tl) {
     if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
-    else finv_phase<M, E, p>(x, tw, tl);
+    else finv_phase_lds<M, E, p>(x, tw, tl);
     if constexpr (p > 0) {
         constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
         fexchange<M, E, p, p - 1, reg ? false : pre>(x, row, tl);
@@ -654,23 +710,27 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             for (int h = 1; h < 3; ++h)  // uniform quarter turn
                 fft::psi_quadrant(bre[h - 1][m >> 2], bim[h - 1][m >> 2], ((h == 1 ? ei : ej) * sm) & 3u, cr[h], ci[h]);
             fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
-            double zr, zi;
+            // per row r: K_r = sum_g B_g[r][P] (c_g - 1), g ascending; then
+            // z = D_P K_P + sum_(r != P, ascending) D_r K_r  (own row first).
+            // 16 (K + 1) VALU per slot (k = 1: 32, against 36 for sum_g (c_g - 1) y_g)
+            double kor, koi, kxr[K], kxi[K];
 #pragma unroll
             for (int gg = 0; gg < 3; ++gg) {
-                // y_g = D_P B_g[P][P] + sum_(r != P, ascending) D_r B_g[r][P]  (own row first)
-                double yr, yi;
-                {
-                    const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
-                    fft::cmul(own.x, own.y, Bo.x, Bo.y, yr, yi);
-                }
+                const double c1r = cr[gg] - 1.0, c1i = ci[gg];
+                const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
+                if (gg == 0) fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                else fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
 #pragma unroll
                 for (int q = 0; q < K; ++q) {
                     const double2 Bx = LAT ? gv[gg][1 + q][LAT ? m : 0] : Bc[gg][1 + q];
-                    fft::cmac(oth[q].x, oth[q].y, Bx.x, Bx.y, yr, yi);
+                    if (gg == 0) fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
+                    else fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
                 }
-                if (gg == 0) fft::cmul(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
-                else fft::cmac(yr, yi, cr[gg] - 1.0, ci[gg], zr, zi);
             }
+            double zr, zi;
+            fft::cmul(own.x, own.y, kor, koi, zr, zi);
+#pragma unroll
+            for (int q = 0; q < K; ++q) fft::cmac(oth[q].x, oth[q].y, kxr[q], kxi[q], zr, zi);
             x[m] = make_double2(zr, zi);
             if constexpr (!LAT) {
                 // keep the loads one slot ahead / in their slot, not all hoisted
@@ -759,7 +819,14 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 // ================================================================== host side
 // compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
 // BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
-static bool fft_supported(int K, int N, int E) { return ((K == 1 && N == 2048) || (K == 2 && N == 1024)) && (E == 4 || E == 8); }
+// k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4)
+template <int N, int K, int E>
+constexpr bool fft_shape_ok() {
+    return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
+}
+static bool fft_supported(int K, int N, int E) {
+    return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
+}
 
 template <int N, int K, int E, bool LAT>
 static void fft_attr() {
@@ -782,12 +849,12 @@ void Device::init_fft() {
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
     if (!fft_supported(p_.k, p_.N, fft_e_))
-        throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N) in {(1, 2048), (2, 1024)}, E in {4, 8}");
+        throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N, E) in {(1, 2048, 4), (2, 1024, 4 or 8)}");
     fft_dispatch(p_, [&](auto nc, auto kc) {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
         fft_attr<N, K, 4, true>();
         fft_attr<N, K, 4, false>();
-        fft_attr<N, K, 8, false>();
+        if constexpr (fft_shape_ok<N, K, 8>()) fft_attr<N, K, 8, false>();
     });
 
     fft::Tables T(p_.N);
@@ -811,6 +878,7 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
     // lane tl's element m is slot idx<LAST>(tl, m), so each load of a wave is 1 KB contiguous
     std::vector<fft::c64> lanes(four.size());
     for (int E : {8, 4}) {
+        if (!fft_supported(p_.k, N, E)) continue;
         const int T = M / E;
         int e = 0;
         while ((1 << e) < E) ++e;
@@ -836,6 +904,7 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
         auto go = [&](auto ec, auto lat) {
             constexpr int E = decltype(ec)::value;
             constexpr bool LAT = decltype(lat)::value;
+            if constexpr (fft_shape_ok<N, K, E>())
             k_blind_rotate_fft<N, K, E, LAT><<<(unsigned)n, fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT>(), s>>>(
                 d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_),
                 (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());

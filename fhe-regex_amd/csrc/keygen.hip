@@ -16,7 +16,8 @@
 //                  2^(64 - pbs_base_log) on coefficient 0 of component r
 //   k_bsk_fourier  one workgroup per polynomial: fold, forward negacyclic FFT in
 //                  LDS (fft.h butterflies, host twiddles), scale 2^-log2(M),
-//                  written in both lane layouts of the blind-rotation kernels
+//                  written in the lane layouts of the blind-rotation kernels
+//                  (E = 4; k = 2 also E = 8)
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -162,7 +163,7 @@ __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict_
     }
     const double scale = 1.0 / (double)M;  // 2^-LOG, exact
     for (int idx = tid; idx < M; idx += 256) {
-        {  // E = 8
+        if (out8) {  // E = 8 (k = 2 only)
             constexpr int E = 8, e = 3, T = M / E, LAST = (LOG + e - 1) / e - 1;
             const int m = idx / T, tl = idx % T;
             const int slot = geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << L8);
@@ -301,11 +302,11 @@ void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
         else k_gen_bsk<1024><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
         KG_CHECK(hipGetLastError());
 
-        // Fourier BSK in both lane layouts
+        // Fourier BSK in the lane layouts of the shapes (E = 4; k = 2 also E = 8)
         for (double** dst : {&d_fbsk_, &d_fbsk4_}) {
             (void)hipFree(*dst);
             *dst = nullptr;
-            KG_CHECK(hipMalloc(dst, 16 * bsk_polys * M));
+            if (dst == &d_fbsk4_ || p_.k == 2) KG_CHECK(hipMalloc(dst, 16 * bsk_polys * M));
         }
         const int LOG = __builtin_ctz(M);
         const int L8 = geo_lo(LOG, 3, (LOG + 2) / 3 - 1), L4 = geo_lo(LOG, 2, (LOG + 1) / 2 - 1);

@@ -305,8 +305,40 @@ static void fft_forward(const fft_plan* F, cplx* z) {
         }
     }
 }
-/* inverse: (A, B) -> (A + B, conj(c) (A - B)), slot order -> natural, times M */
+/* inverse radix-4 group (fft.h inv_r4): stages s1 = 2p + 1 then s0 = 2p on x0..x3
+ * (x1 = x0's stage-s1 partner, x2 its stage-s0 partner); stage s1's twiddles are ca
+ * and i ca (exactly: split-tree siblings), stage s0's c:
+ *   a = x0 + x1, d1 = x0 - x1, b = x2 + x3, d2 = x2 - x3, t1 = d1 - i d2, t2 = d1 + i d2,
+ *   x0 <- a + b, x1 <- conj(ca) t1, x2 <- conj(c) (a - b), x3 <- conj(c ca) t2 */
+static inline void conj_mul(double wr, double wi, double dr, double di, double* zr, double* zi) {
+    *zr = fma(wr, dr, wi * di);
+    *zi = fma(wr, di, -(wi * dr));
+}
+static void inv_r4(cplx* x0, cplx* x1, cplx* x2, cplx* x3, cplx c, cplx ca, cplx cc) {
+    double ar = x0->re + x1->re, ai = x0->im + x1->im, d1r = x0->re - x1->re, d1i = x0->im - x1->im;
+    double br = x2->re + x3->re, bi = x2->im + x3->im, d2r = x2->re - x3->re, d2i = x2->im - x3->im;
+    double t1r = d1r + d2i, t1i = d1i - d2r, t2r = d1r - d2i, t2i = d1i + d2r;
+    double er = ar - br, ei = ai - bi;
+    x0->re = ar + br; x0->im = ai + bi;
+    conj_mul(ca.re, ca.im, t1r, t1i, &x1->re, &x1->im);
+    conj_mul(c.re, c.im, er, ei, &x2->re, &x2->im);
+    conj_mul(cc.re, cc.im, t2r, t2i, &x3->re, &x3->im);
+}
+/* inverse: (A, B) -> (A + B, conj(c) (A - B)), slot order -> natural, times M;
+ * for even log2 M the stages go in radix-4 pairs (2p + 1, 2p) */
 static void fft_inverse(const fft_plan* F, cplx* z) {
+    if (F->LOG % 2 == 0) {
+        for (int s0 = F->LOG - 2; s0 >= 0; s0 -= 2) {
+            int s1 = s0 + 1, h1 = F->M >> (s1 + 1), h0 = 2 * h1;
+            for (int b = 0; b < (1 << s0); b++) {
+                cplx c = F->tw[(1 << s0) + b], ca = F->tw[(1 << s1) + 2 * b], cc;
+                c_mul(c.re, c.im, ca.re, ca.im, &cc.re, &cc.im);
+                for (int j = b * 2 * h0; j < b * 2 * h0 + h1; j++)
+                    inv_r4(&z[j], &z[j + h1], &z[j + h0], &z[j + h0 + h1], c, ca, cc);
+            }
+        }
+        return;
+    }
     for (int s = F->LOG - 1; s >= 0; s--) {
         int h = F->M >> (s + 1);
         for (int b = 0; b < (1 << s); b++) {
@@ -573,6 +605,7 @@ void* or_bsk_prepare(const or_params* P, const uint64_t* bsk) {
     or_bsk* K = (or_bsk*)calloc(1, sizeof(or_bsk));
     K->P = *P;
     if (P->ring == 1) {
+        if (P->k + 1 > 8) { free(K); return NULL; }
         K->FP = fft_plan_make(P->N);
         int M = P->N / 2;
         size_t polys = bsk_ggsw(P) * (P->k + 1) * (P->k + 1);
@@ -713,18 +746,20 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
                     quarter_turns(qv.re, qv.im, kk / (uint32_t)(N / 2), &cr[h], &ci[h]);
                 }
                 c_mul(cr[1], ci[1], cr[2], ci[2], &cr[0], &ci[0]);
-                double zr = 0, zi = 0;
-                for (int g = 0; g < 3; g++) {
-                    const cplx* G = K->bsk_f + ((size_t)(i / 2) * 3 + g) * kp1 * kp1 * M;
-                    /* y_g = sum_r D_r G_g[r][c], the r = c term first */
-                    double yr, yi;
-                    c_mul(D[c * M + t].re, D[c * M + t].im, G[(c * kp1 + c) * M + t].re, G[(c * kp1 + c) * M + t].im, &yr, &yi);
-                    for (size_t r = 0; r < kp1; r++)
-                        if (r != c)
-                            c_mac(D[r * M + t].re, D[r * M + t].im, G[(r * kp1 + c) * M + t].re, G[(r * kp1 + c) * M + t].im, &yr, &yi);
-                    if (g == 0) c_mul(yr, yi, cr[g] - 1.0, ci[g], &zr, &zi);
-                    else c_mac(yr, yi, cr[g] - 1.0, ci[g], &zr, &zi);
-                }
+                /* per row r: K_r = sum_g G_g[r][c] (c_g - 1), g ascending; then
+                 * z = D_c K_c + sum_(r != c, ascending) D_r K_r (the r = c term first) */
+                double kr[8], ki[8]; /* k + 1 <= 8 (or_bsk_prepare) */
+                for (size_t r = 0; r < kp1; r++)
+                    for (int g = 0; g < 3; g++) {
+                        const cplx* G = K->bsk_f + ((size_t)(i / 2) * 3 + g) * kp1 * kp1 * M;
+                        const cplx B = G[(r * kp1 + c) * M + t];
+                        if (g == 0) c_mul(B.re, B.im, cr[g] - 1.0, ci[g], &kr[r], &ki[r]);
+                        else c_mac(B.re, B.im, cr[g] - 1.0, ci[g], &kr[r], &ki[r]);
+                    }
+                double zr, zi;
+                c_mul(D[c * M + t].re, D[c * M + t].im, kr[c], ki[c], &zr, &zi);
+                for (size_t r = 0; r < kp1; r++)
+                    if (r != c) c_mac(D[r * M + t].re, D[r * M + t].im, kr[r], ki[r], &zr, &zi);
                 Z[t].re = zr; Z[t].im = zi;
             }
             fft_inverse(F, Z);
