@@ -133,9 +133,9 @@ class Device {
     int8_t* d_kl_ = nullptr;      // KSK as balanced byte limbs [col*8 + limb][k] (MFMA keyswitch)
     int kl_cols_ = 0;
     bool ks_mfma_ = true;         // FR_KS_MFMA=0: the VALU lincomb+keyswitch kernel
-    int ks_tiles_ = 2048;         // FR_KS_TILES: split K until tiles * split reaches this
     size_t ks_mr4_min_ = 128;     // FR_KS_MR4_MIN: batches from this size use 4 row tiles per wave
-    int ks_mc_ = 0;               // FR_KS_MC=1|2: column tiles per wave in the 4-row-tile shape (0: auto)
+    int ks_mc_ = 0;               // FR_KS_MC=2: two column tiles per wave in the 4-row-tile shape (else one)
+    int ks_split_ = 0;            // FR_KS_SPLIT: K slices (a divisor of kN*ks_level/256; 0: auto)
     int8_t* d_dig_ = nullptr;     // keyswitch digits [rows][kN*ks_level]
     size_t dig_cap_ = 0;
     uint32_t* d_bsk_ = nullptr;  // NTT domain [i][r][c][prime][slot], Montgomery form, scaled by 1/N

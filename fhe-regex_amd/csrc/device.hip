@@ -779,10 +779,16 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
 // and KSK split into 8 balanced byte limbs, KSK = sum_l L_l * 256^l (mod 2^64),
 // L_l in [-128, 128).  Each sum_k D * L_l is an exact i32 GEMM (|.| <= 4 * 128 *
 // 10240 < 2^31) on v_mfma_i32_32x32x32_i8; limbs recombine in the epilogue.
-// Layouts: D [Bp][KD] int8 (Bp = B rounded up to 32, zero rows), L [col*8 + l][KD]
-// int8 (columns padded to a multiple of 4 with zeros).
+// Layouts: D (Bp rows: B rounded up to the wave's row tiles, zero rows) and L (limb
+// column col*8 + l, padded with zero columns) in MFMA fragment order: the operand of
+// (32-row tile, 32-k tile) is 1 KB contiguous, lane r + 32h holding row r, k = 16h..16h+15,
+// so every fragment load of a wave is one fully coalesced 1 KB read.
 typedef int v4i_t __attribute__((ext_vector_type(4)));
 typedef int v16i_t __attribute__((ext_vector_type(16)));
+// byte offset of (row, k) in a fragment-ordered operand with KT = KD / 32 k tiles
+__device__ __forceinline__ size_t ks_frag(int row, int k, int KT) {
+    return ((((size_t)(row >> 5) * KT + (k >> 5)) * 64 + (row & 31) + 32 * ((k >> 4) & 1)) << 4) + (k & 15);
+}
 
 // lincomb + digits: one thread per (gate, input coefficient); the body per gate.
 // The same launch zeroes the mask words of each output row (the MFMA pass
@@ -791,10 +797,10 @@ template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
 k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride, int big,
             int8_t* __restrict__ dig, uint64_t* __restrict__ ks, int ks_n, int ks_stride) {
-    const int g = blockIdx.y;
-    if (g >= B) {  // padding row of the last 32-row tile: zero digits
-        int4* o = (int4*)(dig + (size_t)g * big * KSL);
-        for (int i = blockIdx.x * 256 + threadIdx.x; i < big * KSL / 16; i += gridDim.x * 256) o[i] = int4{0, 0, 0, 0};
+    const int g = blockIdx.y, KT = big * KSL / 32;
+    if (g >= B) {  // padding row of the last row tile: zero digits (16-byte halves of its fragments)
+        for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * KT; i += gridDim.x * 256)
+            *(int4*)(dig + ks_frag(g, 16 * i, KT)) = int4{0, 0, 0, 0};
         return;
     }
     const DevGate& gg = gates[g];
@@ -808,9 +814,8 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
         } else {
             int32_t d[KSL];
             ks_decompose<KSB, KSL>(v, d);
-            int8_t* o = dig + (size_t)g * big * KSL + (size_t)i * KSL;
 #pragma unroll
-            for (int j = 0; j < KSL; ++j) o[j] = (int8_t)d[j];
+            for (int j = 0; j < KSL; ++j) dig[ks_frag(g, i * KSL + j, KT)] = (int8_t)d[j];
         }
     }
 }
@@ -830,12 +835,13 @@ k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, 
     const int g0 = blockIdx.x * 32 * MR;
     const int lcw = (blockIdx.y * 4 + w) * 32 * MC;  // first limb-column of this wave's MC column tiles
     if (lcw >= nlc) return;  // whole wave
-    const int kspan = KD / gridDim.z, kb = blockIdx.z * kspan;
-    const int8_t* ap = dig + (size_t)(g0 + r) * KD + 16 * h + kb;
+    const int kspan = KD / gridDim.z, kb = blockIdx.z * kspan, KT = KD / 32;
+    // fragment (tile, k) at ((tile * KT + k / 32) * 64 + lane) * 16: one k step of 32 is 1 KB
+    const int8_t* ap = dig + ((size_t)(g0 >> 5) * KT * 64 + lane) * 16 + (size_t)kb * 32;
     const int8_t* bp[MC];
 #pragma unroll
     for (int c = 0; c < MC; ++c)  // a tile past the padded columns re-reads the last one (its result is dropped)
-        bp[c] = kl + (size_t)(min(lcw + 32 * c, nlc - 32) + r) * KD + 16 * h + kb;
+        bp[c] = kl + ((size_t)(min(lcw + 32 * c, nlc - 32) >> 5) * KT * 64 + lane) * 16 + (size_t)kb * 32;
     v16i_t acc[MR][MC];
 #pragma unroll
     for (int t = 0; t < MR; ++t)
@@ -846,9 +852,9 @@ k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, 
 #pragma unroll
         for (int u = 0; u < UN; ++u) {
 #pragma unroll
-            for (int c = 0; c < MC; ++c) b[u][c] = *(const v4i_t*)(bp[c] + k0 + 32 * u);
+            for (int c = 0; c < MC; ++c) b[u][c] = *(const v4i_t*)(bp[c] + (size_t)(k0 + 32 * u) * 32);
 #pragma unroll
-            for (int t = 0; t < MR; ++t) a[u][t] = *(const v4i_t*)(ap + (size_t)t * 32 * KD + k0 + 32 * u);
+            for (int t = 0; t < MR; ++t) a[u][t] = *(const v4i_t*)(ap + (size_t)t * KD * 32 + (size_t)(k0 + 32 * u) * 32);
         }
 #pragma unroll
         for (int u = 0; u < UN; ++u)
@@ -882,9 +888,10 @@ k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, 
     }
 }
 
-// KSK (u64 [k][t], t <= n) -> balanced byte limbs [t*8 + l][k]
+// KSK (u64 [k][t], t <= n) -> balanced byte limbs, limb column t*8 + l, fragment order
 __global__ void __launch_bounds__(256) k_ksk_limbs(const uint64_t* __restrict__ ksk, int KD, int ncols, int nlc,
                                                    int8_t* __restrict__ kl) {
+    const int KT = KD / 32;
     const int k = blockIdx.x * 256 + threadIdx.x;
     const int t = blockIdx.y;
     if (k >= KD) return;
@@ -897,14 +904,14 @@ __global__ void __launch_bounds__(256) k_ksk_limbs(const uint64_t* __restrict__ 
             v -= 256;
             x += 1;
         }
-        if (t * 8 + l < nlc) kl[(size_t)(t * 8 + l) * KD + k] = (int8_t)v;
+        if (t * 8 + l < nlc) kl[ks_frag(t * 8 + l, k, KT)] = (int8_t)v;
     }
 }
 
-// linear combination into a slot (no bootstrap): NOT of a boolean
-__global__ void __launch_bounds__(256) k_linear(const DevGate* __restrict__ g, uint64_t* __restrict__ arena,
-                                                int slot_stride, int len) {
-    const DevGate gg = *g;
+// linear combination into a slot (no bootstrap): NOT of a boolean, a match's final
+// affine map.  The gate travels as a kernel argument (no staging copy before the launch).
+__global__ void __launch_bounds__(256) k_linear(const DevGate gg, uint64_t* __restrict__ arena, int slot_stride,
+                                                int len) {
     uint64_t* out = arena + (size_t)gg.out_slot[0] * slot_stride;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < len; t += gridDim.x * 256) {
         uint64_t v = (t == len - 1) ? ((uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1)) : 0;
@@ -980,9 +987,9 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_SMALL_LANE_ELEMS")) e_small_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_SMALL_BATCH")) small_batch_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_KS_MFMA")) ks_mfma_ = std::atoi(ev) != 0;
-    if (const char* ev = std::getenv("FR_KS_TILES")) ks_tiles_ = std::max(1, std::atoi(ev));
     if (const char* ev = std::getenv("FR_KS_MR4_MIN")) ks_mr4_min_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_KS_MC")) ks_mc_ = std::atoi(ev);
+    if (const char* ev = std::getenv("FR_KS_SPLIT")) ks_split_ = std::atoi(ev);
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -1215,14 +1222,15 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         k_ks_digits<3, 5><<<dim3(8, (unsigned)bp), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
                                                                       p_.big(), d_dig_, d_ks, p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
-        // column tiles per wave (A-fragment reuse; auto: two from 512 gates, where the
-        // traffic of re-read digit rows dominates: 178 -> 157 us at 512, 609 -> 472 us at 2048)
-        const int MC = MR != 4 ? 1 : ks_mc_ == 1 || ks_mc_ == 2 ? ks_mc_ : n >= 512 ? 2 : 1;
-        // split K so that small batches still put ~2 waves on every SIMD
-        const int tiles = (int)(bp / (32 * MR)) * (kl_cols_ / 32);
-        const int target = MC == 2 && ks_tiles_ == 2048 ? 8192 : ks_tiles_;
-        int split = 1;
-        while (split < 16 && tiles * split < target && (KD / 256) % (split * 2) == 0) split *= 2;
+        // column tiles per wave: 1 (FR_KS_MC=2 shares each digit fragment between two; with
+        // fragment-ordered operands that no longer pays: 512 gates 121 -> 103 us at 1)
+        const int MC = MR == 4 && ks_mc_ == 2 ? 2 : 1;
+        // K slices (partial sums meet in 64-bit atomics, so more slices cost atomic traffic):
+        // 8 for one row tile per wave, 5 for four (tools/ks_sweep.sh: 1-17 gates ~31 us,
+        // 254 gates 75 -> 61 us against 8); a divisor of KD / 256
+        int split = MR == 1 ? 8 : 5;
+        while ((KD / 256) % split) --split;
+        if (ks_split_ > 0 && (KD / 256) % ks_split_ == 0) split = ks_split_;
         const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)((kl_cols_ + 128 * MC - 1) / (128 * MC)), (unsigned)split);
         if (MR == 4 && MC == 2)
             k_ks_mfma<4, 2><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
@@ -1345,7 +1353,14 @@ void* Device::take_event() {
         event_pool_.pop_back();
         return e;
     }
-    hipEvent_t ev;
+    // timing-only events (read after a stream sync): a device-scope release instead of
+    // the system-scope fence, so recording one between two launches costs no cache
+    // writeback (with the default fence each record opened a ~5 us gap in the level chain)
+    // (the first flag set this runtime accepts)
+    hipEvent_t ev = nullptr;
+    for (unsigned fl : {(unsigned)hipEventReleaseToDevice, (unsigned)hipEventDisableSystemFence, (unsigned)hipEventDefault})
+        if (hipEventCreateWithFlags(&ev, fl) == hipSuccess) return ev;
+        else (void)hipGetLastError();
     HIP_CHECK(hipEventCreate(&ev));
     return ev;
 }
@@ -1367,10 +1382,7 @@ void Device::resolve_timers() {
 }
 
 void Device::run_linear(const DevGate& g) {
-    ensure_batch(1);
-    std::memcpy(stage_acquire(), &g, sizeof g);
-    stage_copy(1);
-    k_linear<<<(p_.lwe_len() + 255) / 256, 256, 0, STREAM>>>(d_gates_, d_arena_, p_.slot_stride(), p_.lwe_len());
+    k_linear<<<(p_.lwe_len() + 255) / 256, 256, 0, STREAM>>>(g, d_arena_, p_.slot_stride(), p_.lwe_len());
     HIP_CHECK(hipGetLastError());
 }
 

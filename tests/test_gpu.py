@@ -378,6 +378,26 @@ def test_plan_cache_replays_bit_identical(gctx):
         gctx.release(h)
 
 
+def test_profiling_timers(gctx):
+    """Profiling mode (bench.py's timed region): per-level KS / BR event timers
+    accumulate one launch per level and the match result is unchanged."""
+    hs = gctx.upload_radix(gctx.encrypt_str("xxabcxxxxxxxxxxxxxxx", seed=14))
+    ref, _ = gctx.has_match(hs, "/abc/")
+    t0 = gctx.device_timers()
+    gctx.set_profiling(True)
+    try:
+        out, st = gctx.has_match(hs, "/abc/")
+    finally:
+        gctx.set_profiling(False)
+    t1 = gctx.device_timers()
+    assert t1["br_launches"] - t0["br_launches"] == st.levels
+    assert t1["br_gates"] - t0["br_gates"] == st.blind_rotations
+    assert t1["br_ms"] > t0["br_ms"] and t1["ks_ms"] > t0["ks_ms"]
+    assert np.array_equal(gctx.download_radix(out), gctx.download_radix(ref))
+    for h in hs + [ref, out]:
+        gctx.release(h)
+
+
 def test_k2_n1024_params_rns(key_blob, fixture_key):
     """The N=1024 variant on the RNS ring (one GGSW per coefficient): the same
     2048-bit key read as k=2 polynomials of 1024."""
