@@ -105,12 +105,15 @@ __device__ __forceinline__ void ffwd_phase(double2 (&x)[E], const double2* tw, i
 }
 template <int M, int E, int p>
 __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, int tl);
+// (radix-4 phases: cc = c ca from the product table twc, indexed like c)
 template <int M, int E, int p>
-__device__ __forceinline__ void finv_phase_lds(double2 (&x)[E], const double2* tw, int tl) {
+__device__ __forceinline__ void finv_phase_lds(double2 (&x)[E], const double2* tw, const double2* twc, int tl) {
     if constexpr (fradix4<M, E>()) {
-        double2 c, ca, cc;
+        using G = FGeo<M, E>;
+        constexpr int s0 = G::s_begin(p);
+        double2 c, ca;
         ftw_r4<M, E, p>(tw, tl, c, ca);
-        fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+        const double2 cc = (twc + (G::template base<p>(tl) >> (G::LOG - s0)))[(1 << s0) + (G::template moff<p>(0) >> (G::LOG - s0))];
         cinv_r4(x, c, ca, cc);
     } else {
         finv_phase<M, E, p>(x, tw, tl);
@@ -146,6 +149,10 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 // previous step's MAC (the rest across the step's own forward FFT)
 #ifndef FR_LAT_PF
 #define FR_LAT_PF 2
+#endif
+// the same for k = 2 (tools/ab_k2.sh: 0 / 1 / 2 / 3 groups: one bootstrap 1.75 / 1.71 / 1.67 / 1.81 ms)
+#ifndef FR_LAT_PF2
+#define FR_LAT_PF2 2
 #endif
 // latency shape, k = 1: the lane's twiddles in registers (1) or read from LDS (0)
 #ifndef FR_LAT_TWR
@@ -369,13 +376,13 @@ __device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, con
 }
 template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false>
 __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
-                                              const double2* tw, int tl) {
+                                              const double2* tw, const double2* twc, int tl) {
     if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
-    else finv_phase_lds<M, E, p>(x, tw, tl);
+    else finv_phase_lds<M, E, p>(x, tw, twc, tl);
     if constexpr (p > 0) {
         constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
         fexchange<M, E, p, p - 1, reg ? false : pre>(x, row, tl);
-        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl);
+        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, twc, tl);
     }
 }
 
@@ -405,10 +412,20 @@ constexpr int fbr_threads() {
 // blocks, so it serves the N-entry and the N/2-entry (quadrant) table alike.
 __device__ __forceinline__ int psi_slot(int k) { return k ^ ((k >> 6) & 15) ^ ((k >> 5) & 1); }
 
+// twiddles in registers (latency shape, k = 1)
+template <int K, bool LAT>
+constexpr bool fbr_twr() {
+    return LAT && K == 1 && FR_LAT_TWR;
+}
+// radix-4 inverse with LDS twiddles: the product table c ca (M/2 entries, indexed like c)
+template <int N, int K, int E, bool LAT>
+constexpr int fbr_twc_entries() {
+    return fradix4<N / 2, E>() && !fbr_twr<K, LAT>() ? N / 4 : 0;
+}
 template <int N, int K, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
     return 16 * ((LAT ? 2 : 1) * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 +
-                 (LAT ? (size_t)N : (size_t)N / 2)) +
+                 (LAT ? (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
            16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT + 2 * 514;
 }
 // workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
@@ -496,14 +513,16 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     static_assert(!LAT || E == 4, "the latency shape holds a step's GGSW values in registers: E = 4");
     constexpr int T = M / E, NT = (K + 1) * T, LAST = G::NPH - 1, XL = G::XL;
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
-    constexpr bool TWR = LAT && K == 1 && FR_LAT_TWR;  // twiddles in registers
+    constexpr bool TWR = fbr_twr<K, LAT>();  // twiddles in registers
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
     double2* xbuf = fsm;                  // K+1 rows of NP complex: row P at P * NP
     double2* ibuf = LAT ? xbuf + (K + 1) * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
     double2* tw = xbuf + (LAT ? 2 : 1) * (K + 1) * G::NP;  // M forward twiddles
     constexpr int NPSI = LAT ? N : N / 2;
     double2* psi = tw + M;                // psi^k, k < NPSI
-    uint8_t* lut = (uint8_t*)(psi + NPSI);             // 16 * n_out
+    double2* twc = psi + NPSI;            // radix-4 products c ca (fbr_twc_entries)
+    constexpr int NTWC = fbr_twc_entries<N, K, E, LAT>();
+    uint8_t* lut = (uint8_t*)(twc + NTWC);             // 16 * n_out
     uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
     uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
     int* wcnt = (int*)(wterms + 16 * MAX_OUT);
@@ -517,6 +536,13 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const int kind = gates[g].direct;
     for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
     for (int i = tid; i < NPSI; i += NT) psi[psi_slot(i)] = psi_g[i];
+    // twc[2^s0 + b] = tw[2^s0 + b] * tw[2^(s0+1) + 2b] for even s0 (fft::cmul, as the oracle)
+    for (int i = 1 + tid; i < NTWC; i += NT) {
+        const int s0 = 31 - __builtin_clz((unsigned)i), b = i - (1 << s0);
+        if (s0 & 1) continue;
+        const double2 c = tw_g[i], ca = tw_g[(2 << s0) + 2 * b];
+        fft::cmul(c.x, c.y, ca.x, ca.y, twc[i].x, twc[i].y);
+    }
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
@@ -595,7 +621,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // single CU streams ~50 GB/s of key at 3.9 us per step); the others across the
     // step's own forward FFT.  The next unskipped step comes from the table nxt (no
     // control flow around the prefetch, which keeps it after the MAC's last use).
-    constexpr int NPF = LAT && K == 1 ? FR_LAT_PF : 0;  // (k = 2: no VGPR room)
+    constexpr int NPF = LAT ? (K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;
     constexpr bool LATPF = NPF > 0;
     if constexpr (LATPF) {
         for (int t = tid; t <= steps; t += NT) {
@@ -751,7 +777,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
-        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, tl);
+        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, twc, tl);
         FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
