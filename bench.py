@@ -206,9 +206,13 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives (nccl = RCCL over xGMI; gloo only to rehearse ranks sharing one GPU)")
     ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
-    ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "r02", "pmc_summary.json"),
-                    help="PMC summary of the BR kernel (tools/pmc_summary.py)")
+    ap.add_argument("--pmc", default="",
+                    help="PMC summary of the BR kernel (tools/pmc_summary.py); default: profiles/r02/"
+                         "pmc_summary.json at k1n2048, pmc_summary_k2n1024.json at k2n1024")
     args = ap.parse_args()
+    if not args.pmc:
+        args.pmc = os.path.join(REPO, "profiles", "r02",
+                                "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json")
 
     W = WORKLOADS[args.workload]
     pattern = args.pattern or W["pattern"]

@@ -17,5 +17,6 @@ step 400 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fetch" -o run --output-format c
 step 400 rocprofv3 --pmc WRITE_SIZE -d "$out/pmc_write" -o run --output-format csv -- python3 $B > "$out/pmc_write.log" 2>&1
 step 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_INSTS_VALU SQ_ACTIVE_INST_LDS -d "$out/pmc_sq" -o run --output-format csv -- python3 $B > "$out/pmc_sq.log" 2>&1
 step 400 rocprofv3 --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS SQ_INSTS_SALU GRBM_GUI_ACTIVE -d "$out/pmc_lds" -o run --output-format csv -- python3 $B > "$out/pmc_lds.log" 2>&1
-python3 tools/pmc_summary.py "$out" "$out/pmc_summary.json"
+k=1; case " $* " in *k2n1024*) k=2 ;; esac
+python3 tools/pmc_summary.py "$out" "$out/pmc_summary.json" "$k"
 echo done
