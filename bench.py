@@ -388,12 +388,13 @@ def main():
                            args.cpu_match_max_jobs)
     ms_per_step = elapsed / args.steps * 1e3
     ring_name = "fft" if params.ring == F.RING_FFT else "rns"
+    coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
     if world == 1:
         par = "single GPU"
     elif strong:
-        par = f"level-sharded x{world} (job slices per level, RCCL all_gather of each level's LWEs)"
+        par = f"level-sharded x{world} (job slices per level, {coll} all_gather of each level's LWEs)"
     else:
-        par = f"start-offset shards x{world} (RCCL all_gather of the per-rank booleans, OR on rank 0)"
+        par = f"start-offset shards x{world} ({coll} all_gather of the per-rank booleans, OR on rank 0)"
     line = {
         "metric": METRIC,
         "value": total_rot / elapsed,
