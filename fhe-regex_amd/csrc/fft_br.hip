@@ -138,7 +138,7 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 // Latency shape: a lane's twiddles are the same every step (they depend on the
 // lane, the stage and the element only), so they are read from LDS once and
 // kept in registers: LOG * E / 2 complex values, index (s, k-th butterfly of s).
-// phases of the latency shape's forward FFT after which GGSW 1 and 2 are loaded
+// phases of the latency shape's forward FFT after which its 2nd and 3rd non-prefetched GGSW groups load
 #ifndef FR_LAT_LOAD1
 #define FR_LAT_LOAD1 2
 #endif
@@ -638,7 +638,18 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         FBR_STAMP(0);
         // the step's byte offset in the key (uniform: soffset of every load)
         const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
-        if constexpr (LAT && NPF < 1) load_ggsw(0, t);
+        // groups NPF.. of this step: G_TOP at the top of the step, G_L1 / G_L2 after forward
+        // phases FR_LAT_LOAD1 / FR_LAT_LOAD2 (3: none).  k = 1, NPF = 2: the third group at the
+        // top (tools/ab_libs.sh: 1.34 ms; after forward phase 0 / 2 / 3: 1.33 / 1.38 / 1.38 ms;
+        // after the previous inverse: 1.35 ms); k = 2 keeps it after phase 3 (1.67 vs 1.71 ms)
+        constexpr int G_TOP = !LAT ? 3 : (NPF < 2 || K == 1) ? NPF : 3;
+        constexpr int G_L1 = !LAT ? 3 : G_TOP + 1 < 3 ? G_TOP + 1 : 3;
+        constexpr int G_L2 = !LAT ? 3 : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
+        if constexpr (G_TOP < 3) {
+            __builtin_amdgcn_sched_barrier(0);
+            load_ggsw(G_TOP, t);
+            __builtin_amdgcn_sched_barrier(0);
+        }
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
         const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
         constexpr int NB = E / 4;
@@ -674,14 +685,14 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
             if constexpr (LAT) {
                 constexpr int p = decltype(ph)::value;
-                if constexpr (p == FR_LAT_LOAD1 && NPF < 2) {
+                if constexpr (p == FR_LAT_LOAD1 && G_L1 < 3) {
                     __builtin_amdgcn_sched_barrier(0);
-                    load_ggsw(1, t);
+                    load_ggsw(G_L1, t);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if constexpr (p == FR_LAT_LOAD2 && NPF < 3) {
+                if constexpr (p == FR_LAT_LOAD2 && G_L2 < 3) {
                     __builtin_amdgcn_sched_barrier(0);
-                    load_ggsw(2, t);
+                    load_ggsw(G_L2, t);
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
