@@ -320,6 +320,12 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl)
 #ifdef FR_FFT_NOXCHG  // timing experiment only (wrong results): LDS exchanges skipped
         return;
 #endif
+#ifdef FR_FFT_NOXCHG_LOCAL  // timing experiment only: wave-local LDS exchanges skipped
+        if constexpr (fwave_local<M, E, PF, PT>()) return;
+#endif
+#ifdef FR_FFT_NOXCHG_CROSS  // timing experiment only: cross-wave LDS exchanges skipped
+        if constexpr (!fwave_local<M, E, PF, PT>()) return;
+#endif
         constexpr int X = PF < PT ? PF : PT;
         double2* rf = row + G::template at<X>(G::template base<PF>(tl));
         double2* rt = row + G::template at<X>(G::template base<PT>(tl));
