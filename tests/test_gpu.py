@@ -77,9 +77,9 @@ def test_keyswitch_bit_exact(gctx, oracle_k1):
 
 @pytest.mark.parametrize("count", [1, 130, 300, 600])
 def test_keyswitch_batch_sizes_bit_exact(gctx, oracle_k1, count):
-    """MFMA keyswitch paths: split-K single rows (1), 4-row-tile blocking with
-    padding (130 -> 256 rows), larger batches, and two column tiles per wave
-    (600 >= 512, 640 padded rows); random (non-message) masks."""
+    """MFMA keyswitch paths (fragment-ordered operands): one row tile per wave with
+    8 K slices (1), 4-row-tile blocking with padding and 5 K slices (130 -> 256
+    rows, 300, 600 -> 640 rows); random (non-message) masks."""
     rng = np.random.default_rng(count)
     blocks = rng.integers(0, 2**64 - 1, (count, gctx.lwe_len), dtype=np.uint64, endpoint=True)
     got = gctx.dev_keyswitch(blocks)
@@ -229,6 +229,26 @@ def test_config2_abc_64(gctx, planted):
     exp = ro.has_match(s, "/abc/")
     got, st = _config(gctx, s, "/abc/", 2)
     assert got == exp.result and st.ct_ops == exp.ct_ops == 371
+
+
+@pytest.mark.parametrize("planted", [True, False])
+def test_large_content_abc_4096(gctx, planted):
+    """Maximum-size case: 4096 chars (16 x the metric) -> 8192 level-1 bootstraps (four
+    throughput launches' worth, arena and batch growth), content encrypted on the device;
+    the match bit against the plaintext oracle, op counts against the plaintext lowering."""
+    rng = np.random.default_rng(44)
+    s = _printable(rng, 4096).replace("abc", "abd")
+    if planted:
+        s = s[:4000] + "abc" + s[4003:]
+    hs = gctx.encrypt_upload_str(s, seed=45)
+    out, st = gctx.has_match(hs, "/abc/")
+    got = gctx.decrypt_radix(gctx.download_radix(out))
+    assert got == int(planted)
+    pm = F.plain_match(s.encode(), "/abc/", engine=F.ENGINE_AUTO)
+    assert got == pm.result_lowered and (st.ct_ops, st.levels) == (pm.ct_ops, pm.levels)
+    assert st.blind_rotations >= 2 * 4096
+    for h in hs + [out]:
+        gctx.release(h)
 
 
 def test_metric_abc_256(gctx):
