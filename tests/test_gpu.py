@@ -87,6 +87,20 @@ def test_keyswitch_batch_sizes_bit_exact(gctx, oracle_k1, count):
     assert (got == exp).all()
 
 
+def test_keyswitch_two_column_tiles_bit_exact(key_blob, fixture_key, monkeypatch):
+    """The FR_KS_MC=2 keyswitch shape (two column tiles per wave; opt-in) and a forced
+    K split (FR_KS_SPLIT=10), bit-exact against the oracle."""
+    monkeypatch.setenv("FR_KS_MC", "2")
+    monkeypatch.setenv("FR_KS_SPLIT", "10")
+    ctx = F.Context(device=0)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    O = of.Oracle(fixture_key, seed=SEED)
+    rng = np.random.default_rng(600)
+    blocks = rng.integers(0, 2**64 - 1, (600, ctx.lwe_len), dtype=np.uint64, endpoint=True)
+    assert (ctx.dev_keyswitch(blocks) == O.keyswitch(blocks)).all()
+
+
 def test_blind_rotate_bit_exact(gctx, oracle_k1):
     O = oracle_k1
     blocks = O.encrypt_blocks([5, 12, 0], seed=31)
