@@ -309,7 +309,29 @@ __device__ __forceinline__ void fperm_exchange(double2 (&x)[E]) {
     if constexpr (j + 1 < FGeo<M, E>::e) fperm_exchange<M, E, PF, PT, j + 1>(x);
 }
 
-template <int M, int E, int PF, int PT, bool PRE>
+// Cross-wave exchanges that only transpose the element bits with the wave bits (lane bits
+// 6, 7), position by position, with every other lane bit in place: a lane keeps the element
+// whose index equals its wave bits, in the same register (forward 0 -> 1, inverse 1 -> 0 of
+// k = 1), so it writes and reads E - 1 elements instead of E (FR_XKEEP).  Throughput shape
+// only (XK): 512 bootstraps 2.80 -> 2.74 ms, 2048 10.66 -> 10.43 ms; the latency shape lost 3%
+// to the wave-uniform branches (tools/ab_libs.sh)
+#ifndef FR_XKEEP
+#define FR_XKEEP 1
+#endif
+template <int M, int E, int PF, int PT>
+constexpr bool fxkeep_ok() {
+    using G = FGeo<M, E>;
+    if (!FR_XKEEP || (1 << (6 + G::e)) > G::T || PF == PT) return false;
+    for (int b = 0; (1 << b) < G::T; ++b) {
+        if (b >= 6 && b < 6 + G::e) {
+            if (G::lane_bit(PF, b) != G::lo(PT) + (b - 6) || G::lane_bit(PT, b) != G::lo(PF) + (b - 6)) return false;
+        } else if (G::lane_bit(PF, b) != G::lane_bit(PT, b)) {
+            return false;
+        }
+    }
+    return true;
+}
+template <int M, int E, int PF, int PT, bool PRE, bool XK = false>
 __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
     using G = FGeo<M, E>;
     if constexpr (fperm_ok<M, E, PF, PT>()) {
@@ -330,6 +352,17 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl)
         double2* rf = row + G::template at<X>(G::template base<PF>(tl));
         double2* rt = row + G::template at<X>(G::template base<PT>(tl));
         if constexpr (PRE) __syncthreads();
+        if constexpr (XK && fxkeep_ok<M, E, PF, PT>()) {  // the kept element: wave-uniform branches around its store and load
+            const int q = __builtin_amdgcn_readfirstlane((tl >> 6) & (E - 1));
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                if (m != q) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                if (m != q) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
+            return;
+        }
 #pragma unroll
         for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
         if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
@@ -376,7 +409,7 @@ __device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, con
     hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
         constexpr bool pre = !NOPRE && (ffwd_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p + 1>();
-        fexchange<M, E, p, p + 1, reg ? false : pre>(x, row, tl);
+        fexchange<M, E, p, p + 1, reg ? false : pre, !NOPRE>(x, row, tl);
         fforward_from<M, E, p + 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl, hook);
     }
 }
@@ -387,7 +420,7 @@ __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, con
     else finv_phase_lds<M, E, p>(x, tw, twc, tl);
     if constexpr (p > 0) {
         constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
-        fexchange<M, E, p, p - 1, reg ? false : pre>(x, row, tl);
+        fexchange<M, E, p, p - 1, reg ? false : pre, !NOPRE>(x, row, tl);
         finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, twc, tl);
     }
 }
