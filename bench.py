@@ -14,10 +14,14 @@ config5 = /^a{2,8}(bc|de)+[^xyz]$/ on 512 chars (state-merging engine).
 
 N > 1 (one process per GPU, torch.distributed over RCCL):
   --scaling strong (default): the named content length is fixed and ONE match
-    is split across the ranks level by level (fheregex.run_sharded over the
-    fr_shard_* C-ABI): each rank runs a contiguous slice of every level's
-    rotation jobs and the level's output LWEs are all-gathered device to device
-    (RCCL all_gather_into_tensor); rank 0 runs the last level.
+    is split across the ranks (fr_shard_* C-ABI).  --shard closure (default,
+    fheregex.run_closure_sharded): the jobs feeding the top of the circuit are
+    cut into contiguous parts, each rank runs the dependency closure of its part
+    (the circuit is local in the content: a few edge jobs run on two ranks), one
+    all_gather_into_tensor (RCCL, device to device) brings the parts' LWEs to
+    rank 0, which runs the top.  --shard level (fheregex.run_sharded): each rank
+    runs a contiguous slice of every level's jobs and every level's output LWEs
+    are all-gathered.
   --scaling weak: --chars start offsets per GPU (content grows with N); each
     rank matches its start range on the content window those starts read, the
     per-rank booleans are all-gathered device to device and OR-ed on rank 0.
@@ -193,6 +197,10 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
                     help="N>1: strong = the workload's content split across ranks (one match, level-sharded); "
                          "weak = --chars start offsets per GPU")
+    ap.add_argument("--shard", default="closure", choices=["closure", "level"],
+                    help="strong scaling: closure = each rank runs the dependency closure of its part of the "
+                         "circuit's top inputs, one gather of those to rank 0 (fheregex.run_closure_sharded); "
+                         "level = every level split into job slices, all-gathered level by level")
     ap.add_argument("--chars", type=int, default=0, help="content chars (strong: total; weak: per GPU); 0: workload's")
     ap.add_argument("--pattern", default="", help="override the workload's pattern")
     ap.add_argument("--content", default="", choices=["", "printable", "alnum", "letters", "config5"])
@@ -278,12 +286,22 @@ def main():
         gather = F.torch_all_gather()
         if strong:
             plan = F.ShardPlan(ctx, handles, pattern)
+            sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
+            runs, _, top = F.closure_parts(sched, world)
+            closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
+            closure_rot[0] += sum(b - a for rl in top for a, b in rl)
 
     def step():
         """one match; returns (result handle on rank 0 or None, rotations run by this rank)"""
         if world == 1:
             out, st = ctx.has_match(handles, pattern)
             return out, st.blind_rotations, st
+        if strong and args.shard == "closure":
+            F.run_closure_sharded(plan, sched, world, rank, gather)
+            if rank == 0:  # the match's rotations (jobs two ranks both ran count once)
+                out, st = plan.finish()
+                return out, len(sched.jobs), st
+            return None, 0, plan.stats
         if strong:
             F.run_sharded(plan, world, rank, gather)
             mine = sum(len(range(*F.job_slice(plan.jobs(l), world, rank))) for l in range(plan.levels - 1))
@@ -391,6 +409,9 @@ def main():
     coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
     if world == 1:
         par = "single GPU"
+    elif strong and args.shard == "closure":
+        par = (f"closure-sharded x{world} (each rank runs the dependency closure of its part of the top's inputs, "
+               f"one {coll} all_gather of those LWEs, rank 0 runs the top)")
     elif strong:
         par = f"level-sharded x{world} (job slices per level, {coll} all_gather of each level's LWEs)"
     else:
@@ -417,6 +438,7 @@ def main():
         "lut_outputs_per_match": float(st.pbs) if world == 1 or strong else None,
         "levels": st.levels,
         "host_ms_per_match": host_ms / args.steps if world == 1 else None,
+        "rotations_run_per_rank": closure_rot if world > 1 and strong and args.shard == "closure" else None,
         "first_call": first_call,
         "result_decrypted": result,
         "result_expected": expected,

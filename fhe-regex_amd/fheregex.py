@@ -576,6 +576,117 @@ def run_sharded(ex, world: int, rank: int, all_gather):
     return gathered
 
 
+def _runs(idx) -> List[Tuple[int, int]]:
+    """maximal contiguous [a, b) runs of a sorted index list"""
+    out = []
+    for i in idx:
+        if out and out[-1][1] == i:
+            out[-1] = (out[-1][0], i + 1)
+        else:
+            out.append((i, i + 1))
+    return out
+
+
+def closure_parts(S: "Schedule", world: int):
+    """Dependency-closure sharding of one match schedule (fr_schedule_match).
+
+    The top of the circuit (the last level, widened downwards while it is fed by
+    too few jobs to split evenly over `world` ranks) runs on rank 0; the jobs that feed it (the frontier)
+    are cut into `world` contiguous parts, and rank r runs the transitive closure
+    of its part (every job its part depends on, level by level; a job two parts
+    need runs on both ranks).  Only the frontier outputs travel, once, to rank 0.
+    The regex circuit is local in the content (a start's branch reads the
+    characters after it, engine.rs:45-214), so a contiguous part's closure is a
+    contiguous window of each level and the duplicated work is the few jobs at
+    the window edges.
+
+    Returns (runs, frontier, top): runs[r][l] = [(a, b), ...] job runs of level l
+    that rank r executes before the gather; frontier[r] = [(l, a, b), ...] the
+    runs of rank r's frontier part, in gather order; top[l] = the runs rank 0
+    executes after the gather."""
+    nl = len(S.level_off) - 1
+    level = []
+    for l in range(nl):
+        level += [l] * (S.level_off[l + 1] - S.level_off[l])
+    prod = {}
+    for gi, j in enumerate(S.jobs):
+        for f in range(j.n_out):
+            prod[j.out_gate[f]] = gi
+
+    def producers(js):
+        return {prod[S.jobs[gi].in_ref[q]] for gi in js for q in range(S.jobs[gi].n_in) if S.jobs[gi].in_ref[q] >= 0}
+
+    def by_level(js):
+        per = [[] for _ in range(nl)]
+        for gi in sorted(js):
+            per[level[gi]].append(gi - S.level_off[level[gi]])
+        return per
+
+    top = set(range(S.level_off[nl - 1], S.level_off[nl])) if nl else set()
+    front = producers(top) - top
+    # widen while some rank would get no part, or the parts are uneven and few
+    while 0 < len(front) and (len(front) < world or (len(front) % world and len(front) < 4 * world)):
+        wider = producers(top | front) - top - front
+        if len(wider) <= len(front):
+            break
+        top |= front
+        front = wider
+    front = sorted(front)
+    runs, frontier = [], []
+    for r in range(world):
+        a, b = job_slice(len(front), world, r)
+        part = front[a:b]
+        need, stack = set(), list(part)
+        while stack:
+            gi = stack.pop()
+            if gi in need:
+                continue
+            need.add(gi)
+            stack += list(producers([gi]))
+        runs.append([_runs(x) for x in by_level(need)])
+        frontier.append([(l, x, y) for l, xs in enumerate(by_level(part)) for x, y in _runs(xs)])
+    return runs, frontier, [_runs(x) for x in by_level(top)]
+
+
+def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather):
+    """One match over `world` ranks by dependency-closure sharding (closure_parts):
+    no exchange until the top of the circuit, then one all_gather of the frontier
+    LWEs (device to device with torch_all_gather) and rank 0 runs the top.  `ex`
+    is a run_sharded executor whose schedule is S.  Returns the number of
+    gathered LWEs."""
+    import torch
+
+    nl = ex.levels
+    if nl != len(S.level_off) - 1 or any(ex.jobs(l) != S.level_off[l + 1] - S.level_off[l] for l in range(nl)):
+        raise ValueError("executor and schedule disagree")
+    runs, frontier, top = closure_parts(S, world)
+    for l in range(nl):
+        for a, b in runs[rank][l]:
+            ex.run(l, a, b)
+    sizes = [sum(ex.outputs(l, a, b) for l, a, b in frontier[r]) for r in range(world)]
+    if max(sizes, default=0):
+        parts = [ex.export(l, a, b, ex.outputs(l, a, b)).reshape(-1)[:ex.outputs(l, a, b) * ex.lwe_len]
+                 for l, a, b in frontier[rank]]
+        cap = max(sizes) * ex.lwe_len
+        have = sum(p.numel() for p in parts)
+        if have < cap:
+            parts.append(torch.zeros(cap - have, dtype=torch.int64,
+                                     device=parts[0].device if parts else ex.buffer_device()))
+        bufs = all_gather(torch.cat(parts).contiguous())
+        if rank == 0:
+            for r in range(1, world):
+                off = 0
+                for l, a, b in frontier[r]:
+                    n = ex.outputs(l, a, b) * ex.lwe_len
+                    ex.import_(l, a, b, bufs[r][off:off + n])
+                    off += n
+    if rank == 0:
+        for l in range(nl):
+            for a, b in top[l]:
+                ex.run(l, a, b)
+    return sum(sizes)
+
+
 class ShardPlan:
     """fr_shard_* executor for run_sharded: a compiled, device-resident plan of one
     match; buffers are torch CUDA tensors (export / import go device to device)."""
@@ -590,6 +701,7 @@ class ShardPlan:
         _check(lib().fr_shard_plan(ctx.h, arr, len(content), pattern.encode("latin-1"), start_lo, hi, C.byref(h),
                                    C.byref(self.stats)))
         self.h = h
+        self.lwe_len = ctx.lwe_len
         n = C.c_uint32()
         _check(lib().fr_shard_levels(h, C.byref(n)))
         self.levels = n.value
@@ -600,6 +712,10 @@ class ShardPlan:
 
     def jobs(self, level: int) -> int:
         return self._jobs[level]
+
+    def buffer_device(self):
+        import torch
+        return torch.device("cuda", self.ctx.device)
 
     def outputs(self, level: int, a: int, b: int) -> int:
         n = C.c_uint32()

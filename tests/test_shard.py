@@ -82,6 +82,40 @@ def test_job_slices_partition():
             assert F.job_slice(J, world, 0)[1] >= 1 or J == 0  # rank 0 owns a lone job
 
 
+@pytest.mark.parametrize("L,pattern,grammar", [(256, "/abc/", 0), (6, "/abc/", 0), (256, "/^[a-z0-9]+$/", 1),
+                                               (1024, "/the/i", 0), (512, CONFIG5, 0), (40, "/^(ab|cd)+/", 0)])
+def test_closure_parts(L, pattern, grammar):
+    """Dependency-closure sharding: every rank's job set is closed under inputs,
+    the frontier parts partition the jobs feeding the top, the top reads only
+    top or frontier outputs, and the top holds the final output."""
+    S = F.schedule_match(L, pattern, grammar=grammar)
+    nl = len(S.level_off) - 1
+    prod = {g: gi for gi, j in enumerate(S.jobs) for g in j.out_gate[:j.n_out]}
+
+    def ids(runs_by_level):
+        return {S.level_off[l] + i for l, rs in enumerate(runs_by_level) for a, b in rs for i in range(a, b)}
+
+    for world in (1, 2, 3, 8):
+        runs, frontier, top = F.closure_parts(S, world)
+        T = ids(top)
+        assert S.out_gate < 0 or prod[S.out_gate] in T
+        fronts = [{S.level_off[l] + i for l, a, b in fr for i in range(a, b)} for fr in frontier]
+        allfront = set().union(*fronts)
+        assert sum(len(f) for f in fronts) == len(allfront)  # a partition
+        for gi in T:
+            j = S.jobs[gi]
+            assert all(prod[j.in_ref[q]] in T | allfront for q in range(j.n_in) if j.in_ref[q] >= 0)
+        for r in range(world):
+            mine = ids(runs[r])
+            assert fronts[r] <= mine  # (a widened top may also be an input of the frontier: run twice)
+            for gi in mine:
+                j = S.jobs[gi]
+                assert all(prod[j.in_ref[q]] in mine for q in range(j.n_in) if j.in_ref[q] >= 0)
+        if world > 1 and L >= 256:  # the split is balanced to within the edge jobs
+            level0 = [sum(b - a for a, b in runs[r][0]) for r in range(world)]
+            assert max(level0) <= 1.2 * (S.level_off[1] / world) + 8
+
+
 class OracleShardExec:
     """run_sharded executor on the CPU oracle: LWE outputs of a schedule's jobs."""
 
@@ -94,6 +128,9 @@ class OracleShardExec:
 
     def jobs(self, l):
         return self.S.level_off[l + 1] - self.S.level_off[l]
+
+    def buffer_device(self):
+        return torch.device("cpu")
 
     def _jobs(self, l, a, b):
         base = self.S.level_off[l]
@@ -168,8 +205,10 @@ def _rank_main(rank: int, world: int, port: int, q):
             S = F.schedule_match(len(c), pattern)
             ex = OracleShardExec(O, S, O.encrypt_str(c, seed=100 + i))
             gathered = F.run_sharded(ex, world, rank, F.torch_all_gather())
+            ex2 = OracleShardExec(O, S, O.encrypt_str(c, seed=100 + i))
+            F.run_closure_sharded(ex2, S, world, rank, F.torch_all_gather())
             if rank == 0:
-                got.append((ex.result(), gathered))
+                got.append((ex.result(), gathered, ex2.result()))
         if rank == 0:
             q.put(got)
     finally:
@@ -179,7 +218,8 @@ def _rank_main(rank: int, world: int, port: int, q):
 def test_sharded_lwes_gloo():
     """World size 2, gloo: real LWEs all-gathered level by level (config 3 and
     config 5 patterns, anchored); result vs the plaintext oracle and vs the
-    unsharded evaluation of the same schedule, bit for bit."""
+    unsharded evaluation of the same schedule, bit for bit; dependency-closure
+    sharding (one gather of the frontier) gives the same bits."""
     world = 2
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -192,7 +232,7 @@ def test_sharded_lwes_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     O = _oracle()
-    for i, ((content, pattern), (lwe, gathered)) in enumerate(zip(GLOO_CASES, got)):
+    for i, ((content, pattern), (lwe, gathered, lwe_closure)) in enumerate(zip(GLOO_CASES, got)):
         want = ro.has_match(content, pattern).result
         assert int(O.decode16(lwe)[0]) == want, (content, pattern)
         S = F.schedule_match(len(content), pattern)
@@ -200,6 +240,7 @@ def test_sharded_lwes_gloo():
         ex = OracleShardExec(O, S, O.encrypt_str(content.encode(), seed=100 + i))
         F.run_sharded(ex, 1, 0, lambda b: [b])
         assert np.array_equal(ex.result(), lwe)
+        assert np.array_equal(lwe_closure, lwe)  # closure sharding: the same bits
     assert [ro.has_match(c, p).result for c, p in GLOO_CASES] == [1, 0, 1, 0]
 
 
@@ -248,5 +289,43 @@ def test_shard_plan_two_ranks_gpu(key_blob, content, pattern):
     ref, rst = ctxs[0].has_match(hs, pattern)
     assert np.array_equal(got, ctxs[0].download_radix(ref))  # bit-identical to the unsharded match
     assert (st.ct_ops, st.blind_rotations, st.levels) == (rst.ct_ops, rst.blind_rotations, rst.levels)
+    for P in plans:
+        P.free()
+
+
+def _two_rank_closure(ctxs, content, pattern, seed):
+    """run_closure_sharded with both 'ranks' on device 0: rank 1 runs its closure
+    first and its frontier export stands in for the all_gather."""
+    world = len(ctxs)
+    S = F.schedule_match(len(content), pattern)
+    plans = [F.ShardPlan(ctx, ctx.upload_radix(ctx.encrypt_str(content, seed=seed)), pattern) for ctx in ctxs]
+    sent = {}
+
+    for r in range(world - 1, -1, -1):
+        def gather(buf, r=r):
+            sent[r] = buf.clone()
+            return [sent.get(q) for q in range(world)]
+        F.run_closure_sharded(plans[r], S, world, r, gather)
+    out, st = plans[0].finish()
+    return plans, out, st
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("content,pattern", [("bcdefghijklmnopq", CONFIG3), ("aaa" + "bcde" * 6 + "f", CONFIG5),
+                                             ("xxxxxabcxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxx", "/abc/"),
+                                             ("x" * 40, "/abc/")])
+def test_closure_two_ranks_gpu(key_blob, content, pattern):
+    ctxs = []
+    for _ in range(2):
+        ctx = F.Context(device=0)
+        ctx.load_client_key(key_blob)
+        ctx.gen_server_key(SEED)
+        ctxs.append(ctx)
+    plans, out, st = _two_rank_closure(ctxs, content, pattern, seed=23)
+    got = ctxs[0].download_radix(out)
+    assert ctxs[0].decrypt_radix(got) == ro.has_match(content, pattern).result
+    hs = ctxs[0].upload_radix(ctxs[0].encrypt_str(content, seed=23))
+    ref, _ = ctxs[0].has_match(hs, pattern)
+    assert np.array_equal(got, ctxs[0].download_radix(ref))  # bit-identical to the unsharded match
     for P in plans:
         P.free()
