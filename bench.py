@@ -383,6 +383,7 @@ def main():
         probe = {}
         for cnt in [int(x) for x in args.probe.split(",")]:
             hs = [src[i % len(src)] for i in range(cnt)]
+            ctx.dev_bench_pbs(hs, 1)  # warm-up (the first launch of a shape runs on a cold clock)
             br_p, tot_p = ctx.dev_bench_pbs(hs, 2)
             probe[cnt] = {"br_ms": br_p / 2, "total_ms": tot_p / 2}
 
