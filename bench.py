@@ -287,7 +287,8 @@ def main():
         if strong:
             plan = F.ShardPlan(ctx, handles, pattern)
             sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
-            runs, _, top = F.closure_parts(sched, world)
+            cparts = F.closure_parts(sched, world)  # once: the host derivation costs ms per call
+            runs, _, top = cparts
             closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
             closure_rot[0] += sum(b - a for rl in top for a, b in rl)
 
@@ -297,7 +298,7 @@ def main():
             out, st = ctx.has_match(handles, pattern)
             return out, st.blind_rotations, st
         if strong and args.shard == "closure":
-            F.run_closure_sharded(plan, sched, world, rank, gather)
+            F.run_closure_sharded(plan, sched, world, rank, gather, cparts)
             if rank == 0:  # the match's rotations (jobs two ranks both ran count once)
                 out, st = plan.finish()
                 return out, len(sched.jobs), st

@@ -648,18 +648,19 @@ def closure_parts(S: "Schedule", world: int):
     return runs, frontier, [_runs(x) for x in by_level(top)]
 
 
-def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather):
+def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather, parts=None):
     """One match over `world` ranks by dependency-closure sharding (closure_parts):
     no exchange until the top of the circuit, then one all_gather of the frontier
     LWEs (device to device with torch_all_gather) and rank 0 runs the top.  `ex`
-    is a run_sharded executor whose schedule is S.  Returns the number of
-    gathered LWEs."""
+    is a run_sharded executor whose schedule is S; `parts` = closure_parts(S,
+    world), computed once by a caller that repeats the match (it costs
+    milliseconds of host time).  Returns the number of gathered LWEs."""
     import torch
 
     nl = ex.levels
     if nl != len(S.level_off) - 1 or any(ex.jobs(l) != S.level_off[l + 1] - S.level_off[l] for l in range(nl)):
         raise ValueError("executor and schedule disagree")
-    runs, frontier, top = closure_parts(S, world)
+    runs, frontier, top = parts if parts is not None else closure_parts(S, world)
     for l in range(nl):
         for a, b in runs[rank][l]:
             ex.run(l, a, b)
