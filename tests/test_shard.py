@@ -244,6 +244,50 @@ def test_sharded_lwes_gloo():
     assert [ro.has_match(c, p).result for c, p in GLOO_CASES] == [1, 0, 1, 0]
 
 
+CLOSURE4_CASES = [("xyabcz", "/abc/"), ("bcdefg", CONFIG3), ("aabcdef", CONFIG5)]
+
+
+def _closure_rank_main(rank: int, world: int, port: int, q):
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        O = _oracle()
+        got = []
+        for i, (content, pattern) in enumerate(CLOSURE4_CASES):
+            c = content.encode()
+            S = F.schedule_match(len(c), pattern)
+            ex = OracleShardExec(O, S, O.encrypt_str(c, seed=200 + i))
+            F.run_closure_sharded(ex, S, world, rank, F.torch_all_gather(), F.closure_parts(S, world))
+            if rank == 0:
+                got.append(ex.result())
+        if rank == 0:
+            q.put(got)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_closure_sharded_gloo_world4():
+    """World size 4, gloo: closure sharding with uneven and empty parts (short
+    contents), real LWEs; bit-identical to the unsharded evaluation."""
+    world = 4
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_closure_rank_main, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=600)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    O = _oracle()
+    for i, ((content, pattern), lwe) in enumerate(zip(CLOSURE4_CASES, got)):
+        S = F.schedule_match(len(content), pattern)
+        ex = OracleShardExec(O, S, O.encrypt_str(content.encode(), seed=200 + i))
+        F.run_sharded(ex, 1, 0, lambda b: [b])
+        assert np.array_equal(ex.result(), lwe), (content, pattern)
+        assert int(O.decode16(lwe)[0]) == ro.has_match(content, pattern).result
+
+
 # ------------------------------------------------------------------- GPU
 def _two_rank_sharded(ctxs, content, pattern, seed):
     """Both 'ranks' on device 0: each runs its slices; the gather concatenates
