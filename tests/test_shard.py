@@ -266,8 +266,9 @@ def _closure_rank_main(rank: int, world: int, port: int, q):
 
 
 def test_closure_sharded_gloo_world4():
-    """World size 4, gloo: closure sharding with uneven and empty parts (short
-    contents), real LWEs; bit-identical to the unsharded evaluation."""
+    """World size 4, gloo: closure sharding with uneven parts (4, 3, 3, 3) and a
+    top widened below the last level (short contents), real LWEs; bit-identical
+    to the unsharded evaluation."""
     world = 4
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
