@@ -4,7 +4,10 @@
 One step = one homomorphic has_match of the workload's pattern over its
 content (real encryptions under the reference's fixture client key, inputs
 resident in HBM): parse -> enumerate -> record -> lower -> level-scheduled
-KS + blind-rotation launches -> result (repeat matches replay the cached plan).
+KS + blind-rotation launches -> result (repeat matches replay the cached plan;
+`fresh_content` times matches on newly encrypted content, which replay the same
+template plan with the new slots bound).  --matches M: each step is M matches of
+the pattern over M contents in shared launches (fr_has_match_batch).
 
 Workloads (--workload; BASELINE.json configs): metric = /abc/ on 256 printable
 chars with "abc" at 200; config2 = /abc/ on 64 chars (run it with --params
@@ -13,27 +16,32 @@ extension: the reference returns Err); config4 = /the/i on 1024 chars;
 config5 = /^a{2,8}(bc|de)+[^xyz]$/ on 512 chars (state-merging engine).
 
 N > 1 (one process per GPU, torch.distributed over RCCL):
-  --scaling strong (default): the named content length is fixed and ONE match
-    is split across the ranks (fr_shard_* C-ABI).  --shard closure (default,
+  --scaling weak (default): per-GPU work fixed.  --shard matches (default): every
+    rank runs --matches independent matches of the workload on its own content
+    (no data-path collective; the timing all-reduce only).  --shard starts: --chars
+    start offsets per GPU (content grows with N); each rank matches its start range
+    on the content window those starts read, the per-rank booleans are
+    all-gathered device to device and OR-ed on rank 0 (the reference's ct_or fold).
+  --scaling strong: the named content length is fixed and ONE match is split
+    across the ranks (fr_shard_* C-ABI).  --shard closure (default,
     fheregex.run_closure_sharded): the jobs feeding the top of the circuit are
-    cut into contiguous parts, each rank runs the dependency closure of its part
-    (the circuit is local in the content: a few edge jobs run on two ranks), one
-    all_gather_into_tensor (RCCL, device to device) brings the parts' LWEs to
+    cut into contiguous parts, each rank runs the dependency closure of its part,
+    one all_gather_into_tensor (RCCL, device to device) brings the parts' LWEs to
     rank 0, which runs the top.  --shard level (fheregex.run_sharded): each rank
     runs a contiguous slice of every level's jobs and every level's output LWEs
-    are all-gathered.
-  --scaling weak: --chars start offsets per GPU (content grows with N); each
-    rank matches its start range on the content window those starts read, the
-    per-rank booleans are all-gathered device to device and OR-ed on rank 0.
+    are all-gathered.  Per-rank phase times are in `per_rank`.  The circuit's four
+    dependent levels bound this mode.
 
 value = blind rotations executed by all ranks per second of wall time (one
 rotation can serve several LUTs: multi-value bootstrapping; the LUT-output
-rate is reported beside it, never as the value); ms_per_step = match time.
+rate is reported beside it, never as the value); ms_per_step = step time.
 roofline: the blind-rotation kernel on rank 0, HIP events on the library's
-stream over the timed region; algorithmic bytes per bootstrap
-n*(k+1)^2*l*N*8; traffic / compute from the rocprofv3 PMC pass
-of this kernel source (tools/profile.sh -> tools/pmc_summary.py).
-cpu_baseline: the CPU restatement (oracle/, "port") timed on this host.
+stream over the timed region.  The kernel is VALU-bound (f64 FFT): `achieved` =
+algorithmic f64 FLOP per bootstrap (algorithmic_flops_per_pbs) x bootstraps /
+BR time against the FP64 vector peak; the HBM side reports the physical traffic
+(rocprofv3 PMC of this kernel source, tools/profile.sh -> tools/pmc_summary.py)
+per launch time.  cpu_baseline: the CPU restatement (oracle/, "port") timed on
+this host's available cores.
 """
 import argparse
 import hashlib
@@ -51,8 +59,10 @@ import fheregex as F  # noqa: E402
 
 METRIC = "TFHE gate-bootstraps/sec; end-to-end match time for /abc/ on 256-char content"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# measured wave64 v_fma_f64 issue: 54 lane-ops per CU-clock = 0.84 VALU wave-instructions
-# per CU-clock (tools/ubench_f64.hip, profiles/r01/ubench_f64.log)
+FP64_VECTOR_PEAK_TFLOPS = 78.6  # MI355X FP64 vector spec: 256 CUs x 128 FLOP/clk x 2.4 GHz
+# wave64 f64 VALU instructions per CU-clock: spec 1.0 (4 SIMDs x 16 f64 lanes); measured
+# v_fma_f64 issue 54 lane-ops per CU-clock = 0.84 (tools/ubench_f64.hip, profiles/r01/ubench_f64.log)
+VALU_SPEC_PER_CU_CLK = 1.0
 VALU_F64_PEAK = 54.0 / 64.0
 SERVER_KEY_SEED = 42
 CONFIG5 = "/^a{2,8}(bc|de)+[^xyz]$/"
@@ -70,9 +80,39 @@ def algorithmic_bytes_per_pbs(p) -> int:
     return p.n * (p.k + 1) ** 2 * p.pbs_level * p.N * 8
 
 
-def make_content(kind: str, L: int) -> bytes:
+def algorithmic_flops_per_pbs(p) -> int:
+    """f64 FLOP of one blind rotation on the FFT ring: ceil(n/2)
+    unrolled steps, each 2(k+1) complex FFTs of M = N/2 points at 5 M log2 M and
+    the external products with three Fourier GGSWs, (k+1)^2 complex MACs (8 FLOP)
+    per GGSW and slot."""
+    M = p.N // 2
+    per_step = 2 * (p.k + 1) * 5 * M * (M.bit_length() - 1) + 3 * (p.k + 1) ** 2 * 8 * M
+    return ((p.n + 1) // 2) * per_step
+
+
+def available_cores():
+    """CPU threads this process may use: the affinity mask, capped by the cgroup
+    CPU quota and by OMP_NUM_THREADS (the GPU box sets it to its per-GPU CPU share)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            if q != "max":
+                quota = max(1, int(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    omp = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    caps = {"affinity": aff, "cgroup_quota": quota, "omp_num_threads": omp}
+    n = min(x for x in (aff, quota, omp) if x)
+    why = [k for k, v in caps.items() if v == n]
+    return n, dict(caps, capped_by=why[0] if why else "affinity")
+
+
+def make_content(kind: str, L: int, seed: int = 0) -> bytes:
     """Seeded synthetic content of the workload (every workload matches)."""
-    rng = np.random.default_rng(0)
+    rng = np.random.default_rng(seed)
     if kind == "printable":
         c = bytearray(rng.integers(0x20, 0x7F, L, dtype=np.uint8).tobytes())
         at = 200 if L >= 256 else L // 4
@@ -92,7 +132,7 @@ def make_content(kind: str, L: int) -> bytes:
         return bytes(s)
     if kind == "config5":  # a{3}(bc|de)*f: matches /^a{2,8}(bc|de)+[^xyz]$/ for even L
         import random
-        r5 = random.Random(5)
+        r5 = random.Random(5 + seed)
         c = ("aaa" + "".join(r5.choice(["bc", "de"]) for _ in range((L - 4) // 2)) + "f").encode()
         assert len(c) == L, "config5 content needs an even length"
         return c
@@ -128,7 +168,8 @@ def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int
     import oracle_ffi as of
 
     O = of.Oracle(of.load_fixture_key(), seed=SERVER_KEY_SEED, k=params.k, N=params.N, ring=params.ring)
-    threads = O.num_threads()
+    threads, caps = available_cores()
+    O.set_threads(threads)
     lut = [int(v == 1) for v in range(16)]
     blocks = O.encrypt_blocks([i % 4 for i in range(2 * sample)], seed=5)
     gates = [([(2 * i, 1), (2 * i + 1, 4)], 0, lut) for i in range(sample)]
@@ -164,6 +205,9 @@ def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int
         "value_1t": n1 / t1,
         "value_all": rate_all,
         "nproc": os.cpu_count(),
+        "cores_available": caps,
+        "cores_note": f"all available threads: min(affinity, cgroup quota, OMP_NUM_THREADS) = {threads}, "
+                      f"capped by {caps['capped_by']}",
         "model": cpu_model(),
         "match_ms": match["ms"],
         "match": match,
@@ -194,13 +238,15 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="metric", choices=sorted(WORKLOADS))
-    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
-                    help="N>1: strong = the workload's content split across ranks (one match, level-sharded); "
-                         "weak = --chars start offsets per GPU")
-    ap.add_argument("--shard", default="closure", choices=["closure", "level"],
-                    help="strong scaling: closure = each rank runs the dependency closure of its part of the "
-                         "circuit's top inputs, one gather of those to rank 0 (fheregex.run_closure_sharded); "
-                         "level = every level split into job slices, all-gathered level by level")
+    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
+                    help="N>1: weak = per-GPU work fixed (default); strong = the workload's content split across "
+                         "ranks (one match)")
+    ap.add_argument("--shard", default="", choices=["", "matches", "starts", "closure", "level"],
+                    help="weak: matches (default; independent matches per rank, no data-path collective) or starts "
+                         "(start-offset shards + RCCL gather + OR); strong: closure (default; each rank runs the "
+                         "dependency closure of its part of the top's inputs, one gather to rank 0) or level (job "
+                         "slices per level, all-gathered level by level)")
+    ap.add_argument("--matches", type=int, default=1, help="matches per rank per step (fr_has_match_batch)")
     ap.add_argument("--chars", type=int, default=0, help="content chars (strong: total; weak: per GPU); 0: workload's")
     ap.add_argument("--pattern", default="", help="override the workload's pattern")
     ap.add_argument("--content", default="", choices=["", "printable", "alnum", "letters", "config5"])
@@ -211,16 +257,21 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=384, help="gates in the CPU baseline sample (0: skip)")
     ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated throughput probe (0: skip)")
+    ap.add_argument("--fresh-steps", type=int, default=5,
+                    help="N=1: matches on newly encrypted content (encryption outside the timing; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives (nccl = RCCL over xGMI; gloo only to rehearse ranks sharing one GPU)")
-    ap.add_argument("--probe", default="", help="comma-separated batch sizes: blind-rotation ms per launch vs batch")
+    ap.add_argument("--probe", default="1,16,254",
+                    help="comma-separated batch sizes: blind-rotation ms per launch vs batch ('' to skip)")
     ap.add_argument("--pmc", default="",
-                    help="PMC summary of the BR kernel (tools/pmc_summary.py); default: profiles/r02/"
+                    help="PMC summary of the BR kernel (tools/pmc_summary.py); default: profiles/r03/"
                          "pmc_summary.json at k1n2048, pmc_summary_k2n1024.json at k2n1024")
     args = ap.parse_args()
     if not args.pmc:
-        args.pmc = os.path.join(REPO, "profiles", "r02",
+        args.pmc = os.path.join(REPO, "profiles", "r03",
                                 "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json")
+    if args.matches < 1:
+        ap.error("--matches must be >= 1")
 
     W = WORKLOADS[args.workload]
     pattern = args.pattern or W["pattern"]
@@ -232,6 +283,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    strong = args.scaling == "strong" and world > 1
+    shard = args.shard or ("closure" if strong else "matches")
+    if world == 1:
+        shard = "matches"  # one GPU: the plain (or batched) match
+    elif strong != (shard in ("closure", "level")):
+        ap.error(f"--shard {shard} does not belong to --scaling {args.scaling}")
+    if world > 1 and shard != "matches" and args.matches != 1:
+        ap.error("--matches > 1 runs with --shard matches (or N = 1)")
     import torch
 
     dist = None
@@ -264,73 +323,109 @@ def main():
     ctx.set_grammar(grammar)
 
     chars = args.chars or W["chars"]
-    strong = args.scaling == "strong" or world == 1
-    L = chars if strong else chars * world
-    content = make_content(kind, L)
-    expected = F.plain_match(content, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
-    # content each rank holds: strong = all of it; weak = the window its starts read
-    if strong:
-        lo, hi, wlo, whi = 0, L, 0, L
-    else:
+    M = args.matches
+    starts = shard == "starts"
+    L = chars * world if starts else chars
+
+    def plant(m):
+        """content of match m of this rank (weak matches: every rank its own)"""
+        return make_content(kind, L, seed=(rank * M + m if shard == "matches" else 0))
+
+    contents = [plant(m) for m in range(M)]
+    content = contents[0]
+    expected = [F.plain_match(c, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+                for c in contents]
+    # content each rank holds: the window its starts read (start shards), else all of it
+    if starts:
         lo, hi = F.shard_starts(L, world, rank)
         wlo, whi = content_window(L, pattern, lo, hi, grammar, engine, lowering)
-    handles = [F.NULL_CT] * L
-    if whi > wlo:
-        msgs = [(c >> (2 * b)) & 3 for c in content[wlo:whi] for b in range(4)]
-        blocks = ctx.encrypt_blocks(msgs, seed=7, first_block=4 * wlo).reshape(whi - wlo, 4, ctx.lwe_len)
-        for i, h in enumerate(ctx.upload_radix(blocks)):
-            handles[wlo + i] = h
+    else:
+        lo, hi, wlo, whi = 0, L, 0, L
+
+    def encrypt(c, seed):
+        hs = [F.NULL_CT] * L
+        if whi > wlo:
+            msgs = [(ch >> (2 * b)) & 3 for ch in c[wlo:whi] for b in range(4)]
+            blocks = ctx.encrypt_blocks(msgs, seed=seed, first_block=4 * wlo).reshape(whi - wlo, 4, ctx.lwe_len)
+            for i, h in enumerate(ctx.upload_radix(blocks)):
+                hs[wlo + i] = h
+        return hs
+
+    batch = [encrypt(c, 7 + 1000 * rank + m) for m, c in enumerate(contents)]
+    handles = batch[0]
 
     plan = None
-    if world > 1:
+    phase = {}
+    if strong:
         gather = F.torch_all_gather()
-        if strong:
-            plan = F.ShardPlan(ctx, handles, pattern)
-            sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
+        plan = F.ShardPlan(ctx, handles, pattern)
+        sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
+        if shard == "closure":
             cparts = F.closure_parts(sched, world)  # once: the host derivation costs ms per call
             runs, _, top = cparts
             closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
             closure_rot[0] += sum(b - a for rl in top for a, b in rl)
+    elif starts and world > 1:
+        gather = F.torch_all_gather()
 
-    def step():
-        """one match; returns (result handle on rank 0 or None, rotations run by this rank)"""
-        if world == 1:
-            out, st = ctx.has_match(handles, pattern)
-            return out, st.blind_rotations, st
-        if strong and args.shard == "closure":
-            F.run_closure_sharded(plan, sched, world, rank, gather, cparts)
+    def step(times=None):
+        """one step; returns ([result handles] on rank 0 (else []), rotations run by this rank, stats)"""
+        if shard == "matches":
+            if M == 1:
+                out, st = ctx.has_match(handles, pattern)
+                return [out], st.blind_rotations, st
+            outs, st = ctx.has_match_batch(batch, pattern)
+            return outs, st.blind_rotations, st
+        if shard == "closure":
+            F.run_closure_sharded(plan, sched, world, rank, gather, cparts, times=times)
             if rank == 0:  # the match's rotations (jobs two ranks both ran count once)
+                t = time.perf_counter()
                 out, st = plan.finish()
-                return out, len(sched.jobs), st
-            return None, 0, plan.stats
-        if strong:
-            F.run_sharded(plan, world, rank, gather)
+                if times is not None:
+                    times["top_ms"] = times.get("top_ms", 0.0) + (time.perf_counter() - t) * 1e3
+                return [out], len(sched.jobs), st
+            return [], 0, plan.stats
+        if shard == "level":
+            F.run_sharded(plan, world, rank, gather, times=times)
             mine = sum(len(range(*F.job_slice(plan.jobs(l), world, rank))) for l in range(plan.levels - 1))
             if rank == 0:
+                t = time.perf_counter()
                 out, st = plan.finish()
-                return out, mine + plan.jobs(plan.levels - 1), st
-            return None, mine, plan.stats
+                if times is not None:
+                    times["top_ms"] = times.get("top_ms", 0.0) + (time.perf_counter() - t) * 1e3
+                return [out], mine + plan.jobs(plan.levels - 1), st
+            return [], mine, plan.stats
+        # start-offset shards
+        t = time.perf_counter()
         out, st = ctx.has_match(handles, pattern, lo, hi)
         buf = torch.empty(ctx.lwe_len, dtype=torch.int64, device=f"cuda:{device}")
         ctx.export_bool_device([out], buf.data_ptr())
         ctx.release(out)
+        if times is not None:
+            times["starts_ms"] = times.get("starts_ms", 0.0) + (time.perf_counter() - t) * 1e3
+        t = time.perf_counter()
         recv = torch.cat(gather(buf))  # [world * lwe_len] on this GPU
         torch.cuda.synchronize()
+        if times is not None:
+            times["gather_ms"] = times.get("gather_ms", 0.0) + (time.perf_counter() - t) * 1e3
         if rank != 0:
-            return None, st.blind_rotations, st
+            return [], st.blind_rotations, st
+        t = time.perf_counter()
         parts = ctx.import_bool_device(recv.data_ptr(), world)
         res = ctx.or_many(parts)
         for h in parts:
             ctx.release(h)
-        return res, st.blind_rotations + (1 if world <= 15 else 2), st
+        if times is not None:
+            times["or_ms"] = times.get("or_ms", 0.0) + (time.perf_counter() - t) * 1e3
+        return [res], st.blind_rotations + (1 if world <= 16 else 2), st
 
     first_call = None
     for _ in range(args.warmup):
         o, _, st0 = step()
         if first_call is None:  # cold call: parse, record, lower, compile, plan upload
             first_call = {"host_ms": st0.host_ms, "device_ms": st0.device_ms, "plan_cached": st0.plan_cached}
-        if o is not None:
-            ctx.release(o)
+        for h in o:
+            ctx.release(h)
 
     ctx.set_profiling(True)
     t_before = ctx.device_timers()
@@ -338,36 +433,71 @@ def main():
     t0 = time.perf_counter()
     rot_local = 0
     host_ms = 0.0
-    out = None
+    outs = []
     st = None
     for i in range(args.steps):
-        o, rot, st = step()
+        o, rot, st = step(phase)
         rot_local += rot
-        host_ms += st.host_ms if world == 1 else 0.0
-        if o is not None:
-            if i + 1 < args.steps:
-                ctx.release(o)
-            else:
-                out = o
+        host_ms += st.host_ms if shard == "matches" else 0.0
+        if i + 1 < args.steps:
+            for h in o:
+                ctx.release(h)
+        else:
+            outs = o
     barrier()
     elapsed = time.perf_counter() - t0
     t_after = ctx.device_timers()
     ctx.set_profiling(False)
 
+    per_rank = None
     if dist is not None:
         tt = torch.tensor([elapsed, float(rot_local)], dtype=torch.float64, device=coll_dev)
         mx = tt.clone()
         dist.all_reduce(mx[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(tt[1:], op=dist.ReduceOp.SUM)
         elapsed, total_rot = float(mx[0]), float(tt[1])
+        # per-rank diagnosis: wall ms per phase per step, rotations run
+        keys = ["closure_ms", "gather_ms", "top_ms", "slices_ms", "import_ms", "starts_ms", "or_ms"]
+        mine = torch.tensor([phase.get(kk, 0.0) / args.steps for kk in keys] +
+                            [float(rot_local) / args.steps, elapsed * 1e3 / args.steps],
+                            dtype=torch.float64, device=coll_dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        per_rank = []
+        for r, v in enumerate(allr):
+            v = v.cpu().tolist()
+            d = {"rank": r, "rotations_run": v[len(keys)], "step_ms": v[len(keys) + 1]}
+            d.update({kk: round(x, 4) for kk, x in zip(keys, v) if kk in phase or x})
+            per_rank.append(d)
     else:
         total_rot = float(rot_local)
 
     result = None
     if rank == 0:
-        result = ctx.decrypt_radix(ctx.download_radix(out))
-        if result != expected:
-            print(f"WARNING: decrypted result {result} != expected {expected}", file=sys.stderr)
+        result = [ctx.decrypt_radix(ctx.download_radix(o)) for o in outs]
+        exp = expected if shard == "matches" else expected[:1]
+        if result != exp:
+            print(f"WARNING: decrypted results {result} != expected {exp}", file=sys.stderr)
+
+    fresh = None
+    if args.fresh_steps and world == 1 and M == 1:
+        # newly encrypted content every step (device encryption outside the timing): the
+        # template plan is replayed with the new content's slots bound
+        ms, cached, ok = [], [], True
+        for i in range(args.fresh_steps):
+            c = make_content(kind, L, seed=100 + i)
+            hs = ctx.encrypt_upload_str(c, seed=500 + i)
+            torch.cuda.synchronize()
+            t = time.perf_counter()
+            o, stf = ctx.has_match(hs, pattern)
+            ms.append((time.perf_counter() - t) * 1e3)
+            cached.append(stf.plan_cached)
+            exp_f = F.plain_match(c, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+            ok &= ctx.decrypt_radix(ctx.download_radix(o)) == exp_f
+            for h in hs + [o]:
+                ctx.release(h)
+        fresh = {"fresh_content_ms": float(np.mean(ms)), "ms": ms, "plan_cached": cached, "results_ok": bool(ok),
+                 "replay_ms": elapsed / args.steps * 1e3}
 
     kernel = None
     if args.saturate and rank == 0:
@@ -397,11 +527,28 @@ def main():
         return
 
     bpp = algorithmic_bytes_per_pbs(params)
+    fpp = algorithmic_flops_per_pbs(params)
     br_ms = t_after["br_ms"] - t_before["br_ms"]
     br_launches = t_after["br_launches"] - t_before["br_launches"]
     br_gates = t_after["br_gates"] - t_before["br_gates"]
-    achieved_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
+    lat = {kk: t_after[kk] - t_before[kk] for kk in ("lat_br_ms", "lat_launches", "lat_gates")}
+    cus = 256
+
+    def shape_line(ms, launches, gates):
+        """one launch shape: algorithmic TFLOP/s, also per active CU (min(bootstraps, 256) CUs)"""
+        if ms <= 0 or launches == 0:
+            return None
+        tf = gates * fpp / (ms / 1e3) / 1e12
+        active = min(gates / launches, cus)
+        return {"launches": int(launches), "bootstraps_per_launch": gates / launches, "avg_ms": ms / launches,
+                "achieved_tflops": tf, "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
+                "frac_of_active_cus": tf / (FP64_VECTOR_PEAK_TFLOPS * active / cus)}
+
+    achieved_tf = br_gates * fpp / (br_ms / 1e3) / 1e12 if br_ms > 0 else 0.0
+    alg_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
+    br_avg_ms = br_ms / max(br_launches, 1)
     pmc = pmc_figures(params, args.pmc)
+    phys = pmc["traffic"] / (br_avg_ms / 1e3) / 1e9 if pmc and pmc.get("traffic") and br_avg_ms > 0 else None
     cpu = None
     if args.cpu_sample > 0 and world == 1:
         cpu = cpu_baseline(params, content, pattern, grammar, engine, lowering, args.cpu_sample,
@@ -410,14 +557,20 @@ def main():
     ring_name = "fft" if params.ring == F.RING_FFT else "rns"
     coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
     if world == 1:
-        par = "single GPU"
-    elif strong and args.shard == "closure":
+        par = "single GPU" + (f", {M} matches per step in shared launches" if M > 1 else "")
+    elif shard == "matches":
+        par = (f"dp{world}: {M} independent match(es) per rank per step on its own content, no data-path collective "
+               f"(max-over-ranks timing)")
+    elif shard == "closure":
         par = (f"closure-sharded x{world} (each rank runs the dependency closure of its part of the top's inputs, "
                f"one {coll} all_gather of those LWEs, rank 0 runs the top)")
-    elif strong:
+    elif shard == "level":
         par = f"level-sharded x{world} (job slices per level, {coll} all_gather of each level's LWEs)"
     else:
         par = f"start-offset shards x{world} ({coll} all_gather of the per-rank booleans, OR on rank 0)"
+    work = f"{args.workload}: {pattern} on {L} chars" + (f" ({chars} per GPU)" if starts else "")
+    if M > 1 or (world > 1 and shard == "matches"):
+        work += f", {M} match(es) per GPU per step"
     line = {
         "metric": METRIC,
         "value": total_rot / elapsed,
@@ -430,41 +583,61 @@ def main():
         "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "u64",
+        "dtype_note": "LWE/GLWE words are u64 on the 2^64 torus; the blind rotation computes in f64 "
+                      "(negacyclic FFT products and an f64 accumulator, tfhe-rs's own arithmetic class, "
+                      "Cargo.lock:110-114 concrete-fft); keyswitch in exact int8 MFMA limbs",
         "data": "synthetic: seeded content, real encryptions under the reference fixture client key",
-        "config": {"workload": f"{args.workload}: {pattern} on {L} chars" + ("" if strong else f" ({chars} per GPU)"),
-                   "content_chars": L, "params": args.params, "ring": ring_name, "lowering": args.lowering,
-                   "engine": args.engine, "content": kind, "scaling": "strong" if strong else "weak",
-                   "parallelism": par},
+        "config": {"workload": work, "content_chars": L, "matches_per_gpu": M, "params": args.params,
+                   "ring": ring_name, "lowering": args.lowering, "engine": args.engine, "content": kind,
+                   "scaling": "strong" if strong else "weak", "shard": shard, "parallelism": par},
         "match_ms": ms_per_step,
-        "blind_rotations_per_match": total_rot / args.steps,
-        "lut_outputs_per_match": float(st.pbs) if world == 1 or strong else None,
+        "blind_rotations_per_step": total_rot / args.steps,
+        "lut_outputs_per_match": float(st.pbs) / (M if shard == "matches" else 1),
         "levels": st.levels,
-        "host_ms_per_match": host_ms / args.steps if world == 1 else None,
-        "rotations_run_per_rank": closure_rot if world > 1 and strong and args.shard == "closure" else None,
+        "host_ms_per_step": host_ms / args.steps if shard == "matches" else None,
+        "rotations_run_per_rank": closure_rot if shard == "closure" else None,
+        "per_rank": per_rank,
         "first_call": first_call,
+        "fresh_content": fresh,
         "result_decrypted": result,
-        "result_expected": expected,
+        "result_expected": expected if shard == "matches" else expected[:1],
         "keygen_s": t_key,
         "roofline": {
-            "bound": "hbm",
-            "achieved": achieved_gbs,
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": achieved_gbs / HBM_PEAK_GBS,
+            "bound": "valu",
+            "achieved": achieved_tf,
+            "peak": FP64_VECTOR_PEAK_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved_tf / FP64_VECTOR_PEAK_TFLOPS,
             "traffic": pmc["traffic"] if pmc else None,
             "kernel": "k_blind_rotate_fft" if params.ring == F.RING_FFT else "k_blind_rotate",
-            "achieved_is": "algorithmic GGSW bytes (n (k+1)^2 l N 8 per bootstrap) / average BR launch time",
-            "bytes_per_pbs": bpp,
+            "achieved_is": "algorithmic f64 FLOP per bootstrap (ceil(n/2) steps x [2(k+1) FFTs at 5 M log2 M + "
+                           "3 (k+1)^2 complex MACs per slot]) x bootstraps / BR kernel time (HIP events, timed "
+                           "region); peak = FP64 vector spec",
+            "flops_per_pbs": fpp,
             "br_launches": br_launches,
-            "br_avg_ms": br_ms / max(br_launches, 1),
+            "br_avg_ms": br_avg_ms,
             "br_gates_per_launch": br_gates / max(br_launches, 1),
-            "compute": None if not pmc or pmc.get("valu_per_cu_clk") is None else {
-                "bound": "valu",
+            "per_shape": {
+                "latency": shape_line(lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
+                "throughput": shape_line(br_ms - lat["lat_br_ms"], br_launches - lat["lat_launches"],
+                                         br_gates - lat["lat_gates"]),
+            },
+            "valu_issue": None if not pmc or pmc.get("valu_per_cu_clk") is None else {
                 "achieved": pmc["valu_per_cu_clk"],
-                "peak": VALU_F64_PEAK,
-                "unit": "VALU wave-instructions per active-CU clock",
-                "frac": pmc["valu_per_cu_clk"] / VALU_F64_PEAK,
-                "peak_is": "measured wave64 v_fma_f64 issue rate (profiles/r01/ubench_f64.log)",
+                "unit": "VALU wave64 instructions per active-CU clock (SQ_INSTS_VALU, rocprofv3 PMC)",
+                "frac_spec": pmc["valu_per_cu_clk"] / VALU_SPEC_PER_CU_CLK,
+                "frac_measured_peak": pmc["valu_per_cu_clk"] / VALU_F64_PEAK,
+                "peaks": {"spec": VALU_SPEC_PER_CU_CLK, "measured_v_fma_f64": VALU_F64_PEAK},
+            },
+            "hbm": {
+                "physical_GBps": phys,
+                "physical_frac": phys / HBM_PEAK_GBS if phys is not None else None,
+                "physical_is": "PMC HBM bytes per BR launch (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE) / "
+                               "average BR launch time",
+                "algorithmic_GBps": alg_gbs,
+                "algorithmic_is": f"n (k+1)^2 l N 8 = {bpp} B of GGSW per bootstrap x bootstraps / BR time: a "
+                                  "normalisation, not a physical rate -- bootstraps in flight share each step's key "
+                                  "through the XCD's L2, so at >= 512 bootstraps per launch it exceeds the 8 TB/s peak",
             },
             "pmc_source": pmc["source"] if pmc else None,
             "pmc_stale": pmc["stale"] if pmc else None,

@@ -4,6 +4,7 @@
 #include <climits>
 #include <cstdlib>
 #include <map>
+#include <unordered_map>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -247,11 +248,15 @@ static Schedule build_schedule(const std::vector<PGate>& gates, size_t n_content
 
 // A device plan: the schedule with references mapped to arena slots (one slot per
 // program gate).  The slots allocated so far are returned if compilation throws.
+// A template plan (n_refs > 0) keeps its content inputs as references
+// (in_slot = -1 - (4 pos + block)) that a content map bound per call resolves
+// (Device::bind_content), so one plan serves every content of the same shape.
 struct Plan {
     std::vector<DevGate> gates;     // levels concatenated
     std::vector<size_t> level_off;  // level l (0-based): gates [level_off[l], level_off[l+1])
     std::vector<int> slot;          // output slot per program gate
     uint64_t pbs = 0, rotations = 0, levels = 0, max_width = 0;
+    size_t n_refs = 0;              // template plan: content references (4 per position)
     DevGate* d_gates = nullptr;     // device-resident copy (cached plans)
 };
 
@@ -260,7 +265,8 @@ static void free_plan_slots(Device& dev, std::vector<int>& slot) {
         if (s >= 0) dev.free_slot(s), s = -1;
 }
 
-static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs) {
+static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std::vector<fr_ct>& inputs,
+                         bool content_refs = false) {
     Device& dev = ctx->device();
     if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
     auto block_slot = [&](int cb) -> const Block& { return ctx->get(inputs[(size_t)(cb / 4)]).b[cb % 4]; };
@@ -287,9 +293,12 @@ static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std
     P.gates = std::move(S.jobs);
     for (DevGate& d : P.gates) {
         for (int q = 0; q < d.n_in; ++q)
-            d.in_slot[q] = d.in_slot[q] >= 0 ? P.slot[d.in_slot[q]] : block_slot(-1 - d.in_slot[q]).slot;
+            d.in_slot[q] = d.in_slot[q] >= 0 ? P.slot[d.in_slot[q]]
+                           : content_refs   ? d.in_slot[q]
+                                            : block_slot(-1 - d.in_slot[q]).slot;
         for (int f = 0; f < d.n_out; ++f) d.out_slot[f] = P.slot[d.out_slot[f]];
     }
+    P.n_refs = content_refs ? 4 * inputs.size() : 0;
     P.level_off = std::move(S.level_off);
     P.pbs = gates.size();
     P.rotations = P.gates.size();
@@ -303,7 +312,7 @@ static Plan compile_plan(fr_ctx* ctx, const std::vector<PGate>& gates, const std
 static void launch_plan(Device& dev, const Plan& P) {
     for (size_t l = 0; l + 1 < P.level_off.size(); ++l) {
         const size_t a = P.level_off[l], n = P.level_off[l + 1] - a;
-        if (P.d_gates) dev.run_level_resident(P.d_gates + a, P.gates.data() + a, n);
+        if (P.d_gates) dev.run_level_resident(P.d_gates + a, P.gates.data() + a, n, P.n_refs);
         else dev.run_level(P.gates.data() + a, n);
     }
 }
@@ -327,9 +336,9 @@ static std::vector<int> execute_gates(fr_ctx* ctx, const std::vector<PGate>& gat
 
 // result handle of a program: boolean out_const + out_w * gate slot (a linear
 // op, no bootstrap), or trivial.  take_slot: the output gate's slot becomes the
-// result's (else the result is a fresh slot and `slots` stay untouched).
-static fr_ct finish_output(fr_ctx* ctx, int out_gate, int out_w, int out_const, std::vector<int>& slots,
-                           bool take_slot) {
+// result's (else the result is a fresh slot and `slots` stay untouched).  Async:
+// the caller synchronises the stream before handing the result out.
+static fr_ct make_output(fr_ctx* ctx, int out_gate, int out_w, int out_const, std::vector<int>& slots, bool take_slot) {
     HandleRec r;
     r.is_bool = true;
     if (out_gate < 0) {
@@ -348,9 +357,14 @@ static fr_ct finish_output(fr_ctx* ctx, int out_gate, int out_w, int out_const, 
         ctx->device().run_linear(d);
         r.b[0].slot = d.out_slot[0];
     }
+    return ctx->new_handle(r);
+}
+static fr_ct finish_output(fr_ctx* ctx, int out_gate, int out_w, int out_const, std::vector<int>& slots,
+                           bool take_slot) {
+    const fr_ct h = make_output(ctx, out_gate, out_w, out_const, slots, take_slot);
     if (take_slot) free_plan_slots(ctx->device(), slots);
     ctx->device().sync();
-    return ctx->new_handle(r);
+    return h;
 }
 
 static fr_ct run_program(fr_ctx* ctx, const Program& prog, const std::vector<fr_ct>& inputs, fr_match_stats* st) {
@@ -361,15 +375,25 @@ static fr_ct run_program(fr_ctx* ctx, const Program& prog, const std::vector<fr_
 static int cblk(int pos, int blk) { return -(1 + pos * 4 + blk); }
 
 // ------------------------------------------------------------ plan cache
-// The circuit of a match is data-oblivious: the same (pattern, grammar, engine,
-// lowering, multi-value, length, start range) and the same content slots give
-// the same plan.  A cached plan keeps its intermediate slots and a device copy
-// of its gate batches, so a repeat call skips parse -> record -> lower ->
-// compile and the per-level descriptor uploads: it only enqueues the levels.
+// The circuit of a match is data-oblivious: it depends on (pattern, grammar,
+// engine, lowering, multi-value, length, start range, batch size) and on the
+// content's *shape* -- which blocks are trivial and their values, and which
+// positions share a ciphertext (the multi-value merge compares inputs) -- never on
+// the ciphertexts themselves.  A cached plan is a template plan (Plan::n_refs):
+// its content inputs are references that each call binds to the call's arena
+// slots through a content map, so a fresh ciphertext of the same shape replays
+// the plan (the reference re-plans every call, engine.rs:8-42).  A cached plan
+// keeps its intermediate slots and a device copy of its gate batches; a repeat
+// call skips parse -> record -> lower -> compile and the descriptor uploads, and
+// only binds the content and enqueues the levels.  The cache is bounded by entries
+// (LRU, default 8, FR_PLAN_CACHE) and by the intermediate slots it holds (default
+// 2^18 = 4.3 GB at k = 1, FR_PLAN_CACHE_SLOTS); eviction runs before the new plan
+// allocates, and a plan larger than the slot budget runs uncached.
 struct CachedMatch {
     std::string key;
-    std::vector<int32_t> sig;  // per content position and block: slot, -1 - trivial value, or absent / bool markers
+    std::vector<int32_t> sig;  // canonical content shape (content_signature)
     Plan plan;
+    size_t n_gates = 0;        // program gates of one match (copy m's gates start at m * n_gates)
     int32_t out_gate = -1, out_w = 0, out_const = 0;
     uint64_t ct_ops = 0, cache_hits = 0, n_branches = 0;
     uint64_t last_use = 0;
@@ -380,6 +404,8 @@ struct CachedMatch {
 struct fr_plan_cache {
     std::vector<std::unique_ptr<fr::CachedMatch>> entries;
     size_t capacity = 8;
+    size_t slot_cap = (size_t)1 << 18;  // intermediate slots held by all cached plans
+    size_t slots_held = 0;
     uint64_t clock = 0, hits = 0, misses = 0;
 };
 
@@ -387,24 +413,43 @@ namespace fr {
 
 static void drop_cached(fr_ctx* ctx, CachedMatch& e);
 
-static std::string match_key(fr_ctx* ctx, const char* pattern, size_t n, size_t lo, size_t hi) {
+static std::string match_key(fr_ctx* ctx, const char* pattern, size_t n, size_t M, size_t lo, size_t hi) {
     std::string k = std::to_string(ctx->grammar) + "|" + std::to_string(ctx->engine) + "|" +
                     std::to_string(ctx->lowering) + "|" + std::to_string((int)ctx->multi_value) + "|" +
-                    std::to_string(n) + "|" + std::to_string(lo) + "|" + std::to_string(hi) + "|";
+                    std::to_string(n) + "|" + std::to_string(M) + "|" + std::to_string(lo) + "|" + std::to_string(hi) +
+                    "|";
     k += pattern;
     return k;
 }
-static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content, size_t n) {
+// Canonical shape of the content: per position and block, the trivial value
+// (-1 - v), the index of the block's ciphertext in order of first appearance (>= 0:
+// equal indices = the same arena slot), or markers for an absent position / a
+// boolean handle.  Two contents with equal signatures lower, schedule and merge
+// identically.  cmap (if given) receives the content map: block r -> slot (-1: none).
+static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content, size_t n, std::vector<int>* cmap) {
     constexpr int32_t ABSENT = INT32_MIN, BOOL = INT32_MIN + 1;
     std::vector<int32_t> sig;
     sig.reserve(4 * n);
+    if (cmap) cmap->assign(4 * n, -1);
+    std::unordered_map<int, int32_t> first;
     for (size_t q = 0; q < n; ++q) {
         if (content[q] == 0xFFFFFFFFu) {
             sig.insert(sig.end(), 4, ABSENT);
             continue;
         }
         const HandleRec& h = ctx->get(content[q]);
-        for (int b = 0; b < 4; ++b) sig.push_back(h.is_bool ? BOOL : h.b[b].slot >= 0 ? h.b[b].slot : -1 - (int32_t)h.b[b].triv);
+        for (int b = 0; b < 4; ++b) {
+            const int s = h.b[b].slot;
+            if (h.is_bool) {
+                sig.push_back(BOOL);
+            } else if (s < 0) {
+                sig.push_back(-1 - (int32_t)h.b[b].triv);
+            } else {
+                auto it = first.emplace(s, (int32_t)first.size()).first;
+                sig.push_back(it->second);
+            }
+            if (cmap) (*cmap)[4 * q + b] = s;
+        }
     }
     return sig;
 }
@@ -413,11 +458,13 @@ static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content,
 
 fr_ctx::fr_ctx() : plans(new fr_plan_cache) {
     if (const char* ev = std::getenv("FR_PLAN_CACHE")) plans->capacity = (size_t)std::max(0, std::atoi(ev));
+    if (const char* ev = std::getenv("FR_PLAN_CACHE_SLOTS")) plans->slot_cap = (size_t)std::max(0L, std::atol(ev));
 }
 void fr_ctx::clear_plans() {
     if (!plans) return;
     for (auto& e : plans->entries) fr::drop_cached(this, *e);
     plans->entries.clear();
+    plans->slots_held = 0;
 }
 fr_ctx::~fr_ctx() {
     try {
@@ -430,26 +477,44 @@ fr_ctx::~fr_ctx() {
 namespace fr {
 
 static void drop_cached(fr_ctx* ctx, CachedMatch& e) {
+    ctx->plans->slots_held -= std::min(ctx->plans->slots_held, e.plan.slot.size());
     if (!ctx->dev) return;
-    ctx->dev->sync();  // no level of this plan may still be in flight
+    ctx->dev->sync();  // no level of this plan may still be in flight (every match ends synchronised)
     free_plan_slots(*ctx->dev, e.plan.slot);
     ctx->dev->free_gates(e.plan.d_gates);
     e.plan.d_gates = nullptr;
 }
+// drop least-recently-used plans until `entries` and `slots` more fit
+static void evict_for(fr_ctx* ctx, size_t entries, size_t slots) {
+    fr_plan_cache& pc = *ctx->plans;
+    while (!pc.entries.empty() &&
+           (pc.entries.size() + entries > pc.capacity || pc.slots_held + slots > pc.slot_cap)) {
+        size_t v = 0;
+        for (size_t i = 1; i < pc.entries.size(); ++i)
+            if (pc.entries[i]->last_use < pc.entries[v]->last_use) v = i;
+        drop_cached(ctx, *pc.entries[v]);
+        pc.entries.erase(pc.entries.begin() + (long)v);
+    }
+}
 
-static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
-                        fr_match_stats* st) {
+// M independent matches of one pattern over M contents of n positions each
+// (content[m * n + q]): one plan whose program is M copies of the match's lowered
+// program, so every level of the M matches shares its launches (M = 1: has_match).
+static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, const char* pattern, size_t lo,
+                       size_t hi, fr_ct* outs, fr_match_stats* st) {
     double t0 = now_ms();
     pattern = pattern ? pattern : "";
     Device& dev = ctx->device();
     if (!ctx->has_sk || !dev.has_keys()) throw Error(FR_ERR_NO_KEY, "server key not generated");
+    if (M == 0) throw Error(FR_ERR_INVALID, "no matches");
     fr_plan_cache& pc = *ctx->plans;
     CachedMatch* hit = nullptr;
     std::string key;
     std::vector<int32_t> sig;
+    std::vector<int> cmap;
     if (pc.capacity) {
-        key = match_key(ctx, pattern, n, lo, hi);
-        sig = content_signature(ctx, content, n);
+        key = match_key(ctx, pattern, n, M, lo, hi);
+        sig = content_signature(ctx, content, n * M, &cmap);
         for (auto& e : pc.entries)
             if (e->key == key && e->sig == sig) hit = e.get();
     }
@@ -458,41 +523,60 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
     bool cached = hit != nullptr;
     double t1;
     DeviceTimers before = dev.timers();
-    fr_ct out;
     if (hit) {
         ++pc.hits;
         hit->last_use = ++pc.clock;
+        dev.bind_content(cmap.data(), cmap.size());
         t1 = now_ms();
         launch_plan(dev, hit->plan);
         add_plan_stats(hit->plan, &local);
         rec.ct_ops = hit->ct_ops;
         rec.cache_hits = hit->cache_hits;
         rec.n_branches = hit->n_branches;
-        out = finish_output(ctx, hit->out_gate, hit->out_w, hit->out_const, hit->plan.slot, false);
+        for (size_t m = 0; m < M; ++m) {
+            const int og = hit->out_gate < 0 ? -1 : hit->out_gate + (int)(m * hit->n_gates);
+            outs[m] = make_output(ctx, og, hit->out_w, hit->out_const, hit->plan.slot, false);
+        }
+        dev.sync();
     } else {
         ++pc.misses;
         ValueDag dag;
         GrammarScope grammar(ctx->grammar);
         rec = record_has_match_engine(dag, n, pattern, lo, hi, ctx->engine);
         Program prog = lower(dag, rec.root, ctx->lowering);
-        // validate referenced content handles
+        // validate the referenced content handles of every match
         for (auto& g : prog.gates)
             for (auto& in : g.ins)
                 if (in.src < 0) {
-                    size_t q = (size_t)((-in.src - 1) / 4);
-                    if (q >= n || content[q] == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
-                    const HandleRec& h = ctx->get(content[q]);
-                    if (h.is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
+                    const size_t q = (size_t)((-in.src - 1) / 4);
+                    for (size_t m = 0; m < M; ++m) {
+                        const fr_ct c = q < n ? content[m * n + q] : 0xFFFFFFFFu;
+                        if (c == 0xFFFFFFFFu) throw Error(FR_ERR_INVALID, "content position not provided");
+                        if (ctx->get(c).is_bool) throw Error(FR_ERR_INVALID, "content handle is not a radix character");
+                    }
                 }
-        std::vector<fr_ct> inputs(content, content + n);
-        Plan P = compile_plan(ctx, prog.gates, inputs);
-        t1 = now_ms();
+        // M copies: gate g of match m is m * G + g, content block cb of match m is 4 n m + cb
+        const size_t G = prog.gates.size();
+        std::vector<PGate> gates;
+        gates.reserve(G * M);
+        for (size_t m = 0; m < M; ++m)
+            for (const PGate& g0 : prog.gates) {
+                PGate g = g0;
+                for (auto& in : g.ins) in.src = in.src >= 0 ? in.src + (int)(m * G) : in.src - (int)(4 * n * m);
+                gates.push_back(std::move(g));
+            }
+        std::vector<fr_ct> inputs(content, content + n * M);
+        const bool keep = pc.capacity && G && G * M <= pc.slot_cap;
+        if (keep) evict_for(ctx, 1, G * M);  // before the new plan allocates its slots
+        Plan P = compile_plan(ctx, gates, inputs, keep);
         add_plan_stats(P, &local);
-        if (pc.capacity && !P.gates.empty()) {
+        auto out_of = [&](size_t m) { return prog.out_gate < 0 ? -1 : prog.out_gate + (int)(m * G); };
+        if (keep) {
             // keep the plan: its slots stay allocated, its batches go to the device once
             auto e = std::make_unique<CachedMatch>();
             e->key = std::move(key);
             e->sig = std::move(sig);
+            e->n_gates = G;
             e->out_gate = prog.out_gate;
             e->out_w = prog.out_w;
             e->out_const = prog.out_const;
@@ -501,22 +585,21 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
             e->n_branches = rec.n_branches;
             e->last_use = ++pc.clock;
             e->plan = std::move(P);
-            e->plan.d_gates = dev.upload_gates(e->plan.gates.data(), e->plan.gates.size());
-            if (pc.entries.size() >= pc.capacity) {  // evict the least recently used
-                size_t v = 0;
-                for (size_t i = 1; i < pc.entries.size(); ++i)
-                    if (pc.entries[i]->last_use < pc.entries[v]->last_use) v = i;
-                drop_cached(ctx, *pc.entries[v]);
-                pc.entries.erase(pc.entries.begin() + (long)v);
-            }
+            pc.slots_held += e->plan.slot.size();
             CachedMatch& c = *e;
             pc.entries.push_back(std::move(e));
+            c.plan.d_gates = dev.upload_gates(c.plan.gates.data(), c.plan.gates.size(), c.plan.n_refs);
+            dev.bind_content(cmap.data(), cmap.size());
+            t1 = now_ms();
             launch_plan(dev, c.plan);
-            out = finish_output(ctx, c.out_gate, c.out_w, c.out_const, c.plan.slot, false);
+            for (size_t m = 0; m < M; ++m) outs[m] = make_output(ctx, out_of(m), c.out_w, c.out_const, c.plan.slot, false);
         } else {
+            t1 = now_ms();
             launch_plan(dev, P);
-            out = finish_output(ctx, prog.out_gate, prog.out_w, prog.out_const, P.slot, true);
+            for (size_t m = 0; m < M; ++m) outs[m] = make_output(ctx, out_of(m), prog.out_w, prog.out_const, P.slot, true);
+            free_plan_slots(dev, P.slot);
         }
+        dev.sync();
     }
     double t2 = now_ms();
     if (st) {
@@ -537,7 +620,6 @@ static fr_ct match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, const char*
         st->br_launches = after.br_launches - before.br_launches;
         st->br_gates = after.br_gates - before.br_gates;
     }
-    return out;
 }
 
 // eager op programs over input handles (pos 0 = a, pos 1 = b)
@@ -1152,22 +1234,42 @@ int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n) {
 int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, fr_ct* out, fr_match_stats* st) {
     FR_TRY({
         NEED(ctx && out && pattern && (content || !n));
-        *out = match_impl(ctx, content, n, pattern, 0, n, st);
+        match_impl(ctx, content, n, 1, pattern, 0, n, out, st);
     })
 }
 
 int fr_set_plan_cache(fr_ctx* ctx, size_t capacity) {
     FR_TRY({
         NEED(ctx);
-        auto& pc = *ctx->plans;
-        pc.capacity = capacity;
-        while (pc.entries.size() > capacity) {  // drop the least recently used beyond the new capacity
-            size_t v = 0;
-            for (size_t i = 1; i < pc.entries.size(); ++i)
-                if (pc.entries[i]->last_use < pc.entries[v]->last_use) v = i;
-            drop_cached(ctx, *pc.entries[v]);
-            pc.entries.erase(pc.entries.begin() + (long)v);
-        }
+        ctx->plans->capacity = capacity;
+        evict_for(ctx, 0, 0);  // drop the least recently used beyond the new capacity
+    })
+}
+
+int fr_set_plan_cache_slots(fr_ctx* ctx, size_t max_slots) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->plans->slot_cap = max_slots;
+        evict_for(ctx, 0, 0);
+    })
+}
+
+int fr_plan_cache_stats(fr_ctx* ctx, uint64_t* entries, uint64_t* slots, uint64_t* hits, uint64_t* misses) {
+    FR_TRY({
+        NEED(ctx);
+        const fr_plan_cache& pc = *ctx->plans;
+        if (entries) *entries = pc.entries.size();
+        if (slots) *slots = pc.slots_held;
+        if (hits) *hits = pc.hits;
+        if (misses) *misses = pc.misses;
+    })
+}
+
+int fr_has_match_batch(fr_ctx* ctx, const fr_ct* content, size_t n_chars, size_t n_matches, const char* pattern,
+                       fr_ct* out, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && out && pattern && n_matches && (content || !n_chars));
+        match_impl(ctx, content, n_chars, n_matches, pattern, 0, n_chars, out, st);
     })
 }
 
@@ -1175,7 +1277,7 @@ int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n, const char* 
                        fr_ct* out, fr_match_stats* st) {
     FR_TRY({
         NEED(ctx && out && pattern && (content || !n) && lo <= hi);
-        *out = match_impl(ctx, content, n, pattern, lo, hi, st);
+        match_impl(ctx, content, n, 1, pattern, lo, hi, out, st);
     })
 }
 
@@ -1530,6 +1632,17 @@ int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct*
             r.b[0].slot = slots[i];
             out[i] = ctx->new_handle(r);
         }
+    })
+}
+int fr_device_timers_latency(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, uint64_t* br_gates) {
+    FR_TRY({
+        NEED(ctx);
+        Device& dev = ctx->device();
+        dev.sync();
+        const DeviceTimers& t = dev.timers();
+        if (br_ms) *br_ms = t.lat_br_ms;
+        if (br_launches) *br_launches = t.lat_launches;
+        if (br_gates) *br_gates = t.lat_gates;
     })
 }
 int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates) {

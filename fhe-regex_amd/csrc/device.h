@@ -34,6 +34,9 @@ int lut_w_norm2(const uint8_t* lut);
 struct DeviceTimers {
     double br_ms = 0, ks_ms = 0;
     uint64_t br_launches = 0, br_gates = 0, lut_outputs = 0;
+    // the part of the above in latency-shape launches (at most one bootstrap per CU)
+    double lat_br_ms = 0;
+    uint64_t lat_launches = 0, lat_gates = 0;
 };
 
 struct ClientKey;
@@ -75,9 +78,16 @@ class Device {
     // run one dependency level of gates (all independent), async on the stream
     void run_level(const DevGate* gates, size_t n);
     // the same for a batch already resident on the device (upload_gates); `host`
-    // is its host copy (validated when uploaded; read for the profiling counters)
-    void run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n);
-    DevGate* upload_gates(const DevGate* gates, size_t n);  // validated, synchronous
+    // is its host copy (validated when uploaded; read for the profiling counters).
+    // n_refs > 0: the batch reads content references (in_slot = -1 - r, r < n_refs)
+    // through the content map bound last (bind_content, at least n_refs entries)
+    void run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n, size_t n_refs = 0);
+    // validated (content references r < n_refs allowed), synchronous
+    DevGate* upload_gates(const DevGate* gates, size_t n, size_t n_refs = 0);
+    // content map of a template plan: reference r reads arena slot cmap[r] (-1: not
+    // read by the plan).  Stream-ordered: launches enqueued after this call see it,
+    // launches enqueued before it keep the previous map.
+    void bind_content(const int* cmap, size_t n);
     void free_gates(DevGate* d);                            // after the stream drained
     // linear combination without bootstrap (NOT of a boolean): out = offset*2^58 + sum w*in
     void run_linear(const DevGate& g);
@@ -104,7 +114,7 @@ class Device {
     // its previous H2D copy completed (no stream-wide sync between levels)
     DevGate* stage_acquire();
     void stage_copy(size_t n);
-    void validate_gates(const DevGate* gates, size_t n) const;
+    void validate_gates(const DevGate* gates, size_t n, size_t n_refs = 0) const;
     void launch_level(const DevGate* d_gates, const DevGate* host, size_t n);
     // profiling: per-level event triples resolved at sync() (no sync per level)
     void* take_event();
@@ -121,6 +131,13 @@ class Device {
     void stage_slot_list(const int* slots, size_t n);  // -> d_slot_list_ (stream order)
     int* d_slot_list_ = nullptr;
     size_t slot_list_cap_ = 0;
+    // content map (bind_content): device copy (rewritten in stream order), pinned
+    // staging ring, entries bound
+    int* d_cmap_ = nullptr;
+    int* h_cmap_[2] = {nullptr, nullptr};
+    void* cmap_ev_[2] = {nullptr, nullptr};
+    size_t cmap_cap_ = 0, cmap_n_ = 0;
+    int cmap_stage_ = 0;
 
     Params p_;
     int dev_;
@@ -160,7 +177,9 @@ class Device {
     struct PendingTimer {
         void* ev[3];
         size_t gates, outs;
+        bool lat;
     };
+    bool latency_shape(size_t n) const;  // launch_br's shape choice for n bootstraps
     std::vector<PendingTimer> pending_;
     std::vector<void*> event_pool_;
     uint64_t* d_ks_ = nullptr;

@@ -703,11 +703,15 @@ k_ring_mul(const uint64_t* __restrict__ a, const uint64_t* __restrict__ b, const
 // KSK rows are read once per tile, coalesced (64 consecutive u64 per wave).
 constexpr int KS_BT = 32, KS_CT = 64, KS_CH = 32;
 
+// arena slot of a gate input: s >= 0 is a slot; s < 0 a content reference of a
+// template plan, resolved through the bound content map (Device::bind_content)
+__device__ __forceinline__ int arena_slot(int s, const int* __restrict__ cmap) { return s >= 0 ? s : cmap[-1 - s]; }
+
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
 k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
-                    const uint64_t* __restrict__ ksk, int n, int big, int chunks_per_split,
-                    unsigned long long* __restrict__ out, int out_stride) {
+                    const int* __restrict__ cmap, const uint64_t* __restrict__ ksk, int n, int big,
+                    int chunks_per_split, unsigned long long* __restrict__ out, int out_stride) {
     __shared__ int8_t dig[KS_BT][KS_CH][KSL];
     __shared__ DevGate sg[KS_BT];
     const int tid = threadIdx.x;
@@ -717,8 +721,12 @@ k_lincomb_keyswitch(const DevGate* __restrict__ gates, int B, const uint64_t* __
     const int c_begin = blockIdx.z * chunks_per_split * KS_CH;
     const int c_end = min(big, c_begin + chunks_per_split * KS_CH);
     for (int e = tid; e < KS_BT; e += 256) {
-        if (b0 + e < B) sg[e] = gates[b0 + e];
-        else sg[e].n_in = 0, sg[e].offset = 0;
+        if (b0 + e < B) {
+            sg[e] = gates[b0 + e];
+            for (int q = 0; q < sg[e].n_in; ++q) sg[e].in_slot[q] = arena_slot(sg[e].in_slot[q], cmap);
+        } else {
+            sg[e].n_in = 0, sg[e].offset = 0;
+        }
     }
     uint64_t acc[8];
 #pragma unroll
@@ -795,8 +803,9 @@ __device__ __forceinline__ size_t ks_frag(int row, int k, int KT) {
 // subtracts into them with atomics) and the padding digit rows B <= g < gridDim.y.
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(256)
-k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride, int big,
-            int8_t* __restrict__ dig, uint64_t* __restrict__ ks, int ks_n, int ks_stride) {
+k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
+            const int* __restrict__ cmap, int big, int8_t* __restrict__ dig, uint64_t* __restrict__ ks, int ks_n,
+            int ks_stride) {
     const int g = blockIdx.y, KT = big * KSL / 32;
     if (g >= B) {  // padding row of the last row tile: zero digits (16-byte halves of its fragments)
         for (int i = blockIdx.x * 256 + threadIdx.x; i < 2 * KT; i += gridDim.x * 256)
@@ -808,7 +817,8 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
     for (int t = blockIdx.x * 256 + threadIdx.x; t < ks_n; t += gridDim.x * 256) ks[(size_t)g * ks_stride + t] = 0;
     for (int i = blockIdx.x * 256 + threadIdx.x; i <= big; i += gridDim.x * 256) {
         uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
-        for (int q = 0; q < nin; ++q) v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)gg.in_slot[q] * slot_stride + i];
+        for (int q = 0; q < nin; ++q)
+            v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + i];
         if (i == big) {
             ks[(size_t)g * ks_stride + ks_n] = v;  // column n of the output row; the MFMA pass subtracts
         } else {
@@ -975,12 +985,13 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
         HIP_CHECK(hipEventCreate(&ev));
         e = ev;
     }
-    for (auto& e : stage_ev_) {
-        hipEvent_t ev;
-        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-        HIP_CHECK(hipEventRecord(ev, s));  // complete before first use
-        e = ev;
-    }
+    for (auto* evs : {&stage_ev_, &cmap_ev_})
+        for (auto& e : *evs) {
+            hipEvent_t ev;
+            HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIP_CHECK(hipEventRecord(ev, s));  // complete before first use
+            e = ev;
+        }
     // unrolled (k = 1) kernels keep three GGSW rows in registers: E = 8 only
     if (p.bsk_unroll() == 2) e_ = e_small_ = 8;
     if (const char* ev = std::getenv("FR_LANE_ELEMS")) e_ = std::atoi(ev);
@@ -1024,6 +1035,11 @@ Device::~Device() {
         if (h) (void)hipHostFree(h);
     for (auto* e : stage_ev_)
         if (e) (void)hipEventDestroy((hipEvent_t)e);
+    for (auto* e : cmap_ev_)
+        if (e) (void)hipEventDestroy((hipEvent_t)e);
+    (void)hipFree(d_cmap_);
+    for (auto* h : h_cmap_)
+        if (h) (void)hipHostFree(h);
     for (auto& t : pending_)
         for (auto* e : t.ev) (void)hipEventDestroy((hipEvent_t)e);
     for (auto* e : event_pool_) (void)hipEventDestroy((hipEvent_t)e);
@@ -1219,7 +1235,7 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
         if (KD % 16) throw Error(FR_ERR_INVALID, "MFMA keyswitch: digit rows must be whole 16-byte vectors");
-        k_ks_digits<3, 5><<<dim3(8, (unsigned)bp), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(),
+        k_ks_digits<3, 5><<<dim3(8, (unsigned)bp), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_cmap_,
                                                                       p_.big(), d_dig_, d_ks, p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         // column tiles per wave: 1 (FR_KS_MC=2 shares each digit fragment between two; with
@@ -1254,10 +1270,12 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
     splits = (chunks + per - 1) / per;
     if (splits > 1) HIP_CHECK(hipMemsetAsync(d_ks, 0, (size_t)8 * p_.ks_stride() * n, STREAM));
     dim3 grid((unsigned)btiles, (unsigned)ctiles, (unsigned)splits);
-    k_lincomb_keyswitch<3, 5><<<grid, 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_ksk_, p_.n,
-                                                         p_.big(), per, (unsigned long long*)d_ks, p_.ks_stride());
+    k_lincomb_keyswitch<3, 5><<<grid, 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_cmap_, d_ksk_,
+                                                         p_.n, p_.big(), per, (unsigned long long*)d_ks, p_.ks_stride());
     HIP_CHECK(hipGetLastError());
 }
+
+bool Device::latency_shape(size_t n) const { return n <= (p_.ring == FR_RING_FFT ? fft_small_ : small_batch_); }
 
 void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
     if (p_.ring == FR_RING_FFT) {
@@ -1274,7 +1292,7 @@ void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
     HIP_CHECK(hipGetLastError());
 }
 
-void Device::validate_gates(const DevGate* gates, size_t n) const {
+void Device::validate_gates(const DevGate* gates, size_t n, size_t n_refs) const {
     for (size_t i = 0; i < n; ++i) {
         const DevGate& g = gates[i];
         if (g.n_in < 0 || g.n_in > 16 || g.n_out < 1 || g.n_out > MAX_OUT || g.direct < 0 || g.direct > 2 ||
@@ -1282,9 +1300,39 @@ void Device::validate_gates(const DevGate* gates, size_t n) const {
             throw Error(FR_ERR_INVALID, "device gate: bad descriptor");
         for (int f = 0; f < g.n_out; ++f)
             if (g.out_slot[f] < 0 || (size_t)g.out_slot[f] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad output slot");
-        for (int q = 0; q < g.n_in; ++q)
-            if (g.in_slot[q] < 0 || (size_t)g.in_slot[q] >= next_slot_) throw Error(FR_ERR_INVALID, "device gate: bad input slot");
+        for (int q = 0; q < g.n_in; ++q) {
+            const int s = g.in_slot[q];
+            if (s >= 0 ? (size_t)s >= next_slot_ : (size_t)(-1 - (int64_t)s) >= n_refs)
+                throw Error(FR_ERR_INVALID, "device gate: bad input slot");
+        }
     }
+}
+
+void Device::bind_content(const int* cmap, size_t n) {
+    for (size_t i = 0; i < n; ++i)
+        if (cmap[i] < -1 || (cmap[i] >= 0 && (size_t)cmap[i] >= next_slot_))
+            throw Error(FR_ERR_INVALID, "content map: slot out of range");
+    if (n > cmap_cap_) {
+        HIP_CHECK(hipStreamSynchronize(STREAM));  // no launch may still read the old map
+        (void)hipFree(d_cmap_);
+        d_cmap_ = nullptr;
+        for (auto& h : h_cmap_) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+        }
+        size_t cap = cmap_cap_ ? cmap_cap_ : 4096;
+        while (cap < n) cap *= 2;
+        HIP_CHECK(hipMalloc(&d_cmap_, 4 * cap));
+        for (auto& h : h_cmap_) HIP_CHECK(hipHostMalloc(&h, 4 * cap));
+        cmap_cap_ = cap;
+    }
+    cmap_stage_ ^= 1;
+    // the pinned buffer is rewritten only after its previous copy completed
+    HIP_CHECK(hipEventSynchronize((hipEvent_t)cmap_ev_[cmap_stage_]));
+    std::memcpy(h_cmap_[cmap_stage_], cmap, 4 * n);
+    if (n) HIP_CHECK(hipMemcpyAsync(d_cmap_, h_cmap_[cmap_stage_], 4 * n, hipMemcpyHostToDevice, STREAM));
+    HIP_CHECK(hipEventRecord((hipEvent_t)cmap_ev_[cmap_stage_], STREAM));
+    cmap_n_ = n;
 }
 
 void Device::run_level(const DevGate* gates, size_t n) {
@@ -1299,15 +1347,16 @@ void Device::run_level(const DevGate* gates, size_t n) {
     launch_level(d_gates_, gates, n);
 }
 
-void Device::run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n) {
+void Device::run_level_resident(const DevGate* d_gates, const DevGate* host, size_t n, size_t n_refs) {
     if (!n) return;
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    if (n_refs > cmap_n_) throw Error(FR_ERR_INVALID, "template plan: content map not bound");
     ensure_batch(n);
     launch_level(d_gates, host, n);
 }
 
-DevGate* Device::upload_gates(const DevGate* gates, size_t n) {
-    validate_gates(gates, n);
+DevGate* Device::upload_gates(const DevGate* gates, size_t n, size_t n_refs) {
+    validate_gates(gates, n, n_refs);
     DevGate* d = nullptr;
     HIP_CHECK(hipMalloc(&d, sizeof(DevGate) * std::max<size_t>(n, 1)));
     HIP_CHECK(hipMemcpy(d, gates, sizeof(DevGate) * n, hipMemcpyHostToDevice));
@@ -1332,6 +1381,7 @@ void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n)
     if (profiling_) {
         HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[2], STREAM));
         t.gates = n;
+        t.lat = latency_shape(n);
         t.outs = 0;
         for (size_t i = 0; i < n; ++i) t.outs += host[i].n_out;
         pending_.push_back(t);
@@ -1376,6 +1426,11 @@ void Device::resolve_timers() {
         timers_.br_launches += 1;
         timers_.br_gates += t.gates;
         timers_.lut_outputs += t.outs;
+        if (t.lat) {
+            timers_.lat_br_ms += br;
+            timers_.lat_launches += 1;
+            timers_.lat_gates += t.gates;
+        }
         for (auto* e : t.ev) event_pool_.push_back(e);
     }
     pending_.clear();

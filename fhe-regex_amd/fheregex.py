@@ -139,6 +139,11 @@ _SIGS = {
                                      C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "fr_plan_cache_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
+                                      C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+    "fr_has_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_size_t, C.c_char_p,
+                                     C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
     "fr_set_engine": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_set_grammar": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_parse_ex": (C.c_int, [C.c_char_p, C.c_int32, C.c_char_p, C.c_size_t]),
@@ -163,6 +168,8 @@ _SIGS = {
     "fr_import_bool_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32)]),
     "fr_device_timers": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_uint64)]),
+    "fr_device_timers_latency": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                           C.POINTER(C.c_uint64)]),
     "fr_shard_plan": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t,
                                 C.POINTER(C.c_void_p), C.POINTER(MatchStats)]),
     "fr_shard_levels": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
@@ -316,6 +323,15 @@ class Context:
         """Plans kept for repeat has_match calls (0: off, frees the cached plans)."""
         _check(lib().fr_set_plan_cache(self.h, capacity))
 
+    def set_plan_cache_slots(self, max_slots: int):
+        """Bound on the intermediate arena slots held by all cached plans."""
+        _check(lib().fr_set_plan_cache_slots(self.h, max_slots))
+
+    def plan_cache_stats(self):
+        v = [C.c_uint64() for _ in range(4)]
+        _check(lib().fr_plan_cache_stats(self.h, *[C.byref(x) for x in v]))
+        return dict(zip(("entries", "slots", "hits", "misses"), (x.value for x in v)))
+
     def set_profiling(self, on: bool):
         _check(lib().fr_set_profiling(self.h, int(on)))
 
@@ -437,6 +453,20 @@ class Context:
                                             C.byref(out), C.byref(st)))
         return out.value, st
 
+    def has_match_batch(self, contents: Sequence[Sequence[int]], pattern: str):
+        """M independent matches of one pattern over M equal-length contents in
+        shared launches (fr_has_match_batch): ([out handle per match], stats)."""
+        M = len(contents)
+        n = len(contents[0]) if M else 0
+        if any(len(c) != n for c in contents):
+            raise ValueError("has_match_batch: contents must have one length")
+        flat = [h for c in contents for h in c]
+        arr = (C.c_uint32 * max(len(flat), 1))(*flat)
+        out = (C.c_uint32 * max(M, 1))()
+        st = MatchStats()
+        _check(lib().fr_has_match_batch(self.h, arr, n, M, pattern.encode("latin-1"), out, C.byref(st)))
+        return list(out)[:M], st
+
     def export_bool_device(self, hs: Sequence[int], dev_ptr: int):
         arr = (C.c_uint32 * len(hs))(*hs)
         _check(lib().fr_export_bool_device(self.h, arr, len(hs), C.c_void_p(dev_ptr)))
@@ -450,7 +480,10 @@ class Context:
         br, ks = C.c_double(), C.c_double()
         nl, ng = C.c_uint64(), C.c_uint64()
         _check(lib().fr_device_timers(self.h, C.byref(br), C.byref(ks), C.byref(nl), C.byref(ng)))
-        return {"br_ms": br.value, "ks_ms": ks.value, "br_launches": nl.value, "br_gates": ng.value}
+        lb, ll, lg = C.c_double(), C.c_uint64(), C.c_uint64()
+        _check(lib().fr_device_timers_latency(self.h, C.byref(lb), C.byref(ll), C.byref(lg)))
+        return {"br_ms": br.value, "ks_ms": ks.value, "br_launches": nl.value, "br_gates": ng.value,
+                "lat_br_ms": lb.value, "lat_launches": ll.value, "lat_gates": lg.value}
 
     # single-stage device entry points
     def dev_keyswitch(self, lwes: np.ndarray) -> np.ndarray:
@@ -549,7 +582,7 @@ def job_slice(J: int, world: int, rank: int) -> Tuple[int, int]:
     return -(-rank * J // world), -(-(rank + 1) * J // world)
 
 
-def run_sharded(ex, world: int, rank: int, all_gather):
+def run_sharded(ex, world: int, rank: int, all_gather, times=None):
     """Level-sharded evaluation of one match plan (fheregex.h fr_shard_*):
     every level but the last is split into contiguous job slices, each rank runs
     its slice, and the slices' output LWEs are all-gathered so that every rank
@@ -557,22 +590,38 @@ def run_sharded(ex, world: int, rank: int, all_gather):
     on the GPU, or a CPU evaluator in tests) with levels / jobs(l) /
     outputs(l, a, b) / run(l, a, b) / export(l, a, b, cap) -> buffer /
     import_(l, a, b, buffer); all_gather(buffer) returns every rank's buffer in
-    rank order.  Returns the number of gathered LWEs."""
+    rank order.  `times` (a dict) accumulates wall milliseconds per phase: slices
+    (runs + exports, which wait for the device), gather, import, top.  Returns the
+    number of gathered LWEs."""
+    import time
+    clock = time.perf_counter
+
+    def tick(phase, t0):
+        if times is not None:
+            times[phase] = times.get(phase, 0.0) + (clock() - t0) * 1e3
+        return clock()
+
     gathered = 0
     nl = ex.levels
+    t = clock()
     for l in range(nl - 1):
         parts = [job_slice(ex.jobs(l), world, r) for r in range(world)]
         counts = [ex.outputs(l, a, b) for a, b in parts]
         a, b = parts[rank]
         if b > a:
             ex.run(l, a, b)
-        bufs = all_gather(ex.export(l, a, b, max(counts)))
+        send = ex.export(l, a, b, max(counts))
+        t = tick("slices_ms", t)
+        bufs = all_gather(send)
+        t = tick("gather_ms", t)
         for r, (ar, br) in enumerate(parts):
             if r != rank and counts[r]:
                 ex.import_(l, ar, br, bufs[r])
+        t = tick("import_ms", t)
         gathered += sum(counts)
     if rank == 0 and nl:
         ex.run(nl - 1, 0, ex.jobs(nl - 1))
+    tick("top_ms", t)
     return gathered
 
 
@@ -648,15 +697,28 @@ def closure_parts(S: "Schedule", world: int):
     return runs, frontier, [_runs(x) for x in by_level(top)]
 
 
-def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather, parts=None):
+def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather, parts=None, times=None):
     """One match over `world` ranks by dependency-closure sharding (closure_parts):
     no exchange until the top of the circuit, then one all_gather of the frontier
     LWEs (device to device with torch_all_gather) and rank 0 runs the top.  `ex`
     is a run_sharded executor whose schedule is S; `parts` = closure_parts(S,
     world), computed once by a caller that repeats the match (it costs
-    milliseconds of host time).  Returns the number of gathered LWEs."""
+    milliseconds of host time).  `times` (a dict) accumulates this rank's wall
+    milliseconds per phase: closure (its jobs and the export of its frontier, which
+    waits for the device), gather, top (imports and the top's launches; the top's
+    device time lands in the caller's finish).  Returns the number of gathered LWEs."""
+    import time
+
     import torch
 
+    clock = time.perf_counter
+
+    def tick(phase, t0):
+        if times is not None:
+            times[phase] = times.get(phase, 0.0) + (clock() - t0) * 1e3
+        return clock()
+
+    t = clock()
     nl = ex.levels
     if nl != len(S.level_off) - 1 or any(ex.jobs(l) != S.level_off[l + 1] - S.level_off[l] for l in range(nl)):
         raise ValueError("executor and schedule disagree")
@@ -673,7 +735,10 @@ def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather, pa
         if have < cap:
             parts.append(torch.zeros(cap - have, dtype=torch.int64,
                                      device=parts[0].device if parts else ex.buffer_device()))
-        bufs = all_gather(torch.cat(parts).contiguous())
+        send = torch.cat(parts).contiguous()
+        t = tick("closure_ms", t)
+        bufs = all_gather(send)
+        t = tick("gather_ms", t)
         if rank == 0:
             for r in range(1, world):
                 off = 0
@@ -681,10 +746,13 @@ def run_closure_sharded(ex, S: "Schedule", world: int, rank: int, all_gather, pa
                     n = ex.outputs(l, a, b) * ex.lwe_len
                     ex.import_(l, a, b, bufs[r][off:off + n])
                     off += n
+    else:
+        t = tick("closure_ms", t)
     if rank == 0:
         for l in range(nl):
             for a, b in top[l]:
                 ex.run(l, a, b)
+    tick("top_ms", t)
     return sum(sizes)
 
 

@@ -194,14 +194,31 @@ int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* 
                  fr_match_stats* stats);
 /* Same, restricted to start offsets [start_lo, start_hi) — the per-GPU shard of
  * the start-offset partition (the OR over shards equals has_match). */
-/* Plan cache: has_match circuits are data-oblivious, so the lowered, compiled
- * plan of (pattern, grammar, engine, lowering, multi-value, n_chars, start range,
- * content slots) is kept -- its intermediate slots and its device-resident gate
- * batches -- and a repeat call only enqueues its levels.  capacity = plans kept
- * (LRU; default 8, env FR_PLAN_CACHE); 0 disables and frees every cached plan. */
-int fr_set_plan_cache(fr_ctx* ctx, size_t capacity);
 int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
                        size_t start_hi, fr_ct* out, fr_match_stats* stats);
+/* n_matches independent has_match calls of one pattern over n_matches contents
+ * of n_chars each (content[m * n_chars + q], out[m]): the matches' circuits run
+ * as one plan, so each dependency level of all matches shares its launches
+ * (throughput mode; every out[m] is bit-identical to fr_has_match on content m).
+ * stats: ct_ops / cache_hits / n_branches of one match; pbs, blind_rotations of
+ * the batch; levels of one match (= of the batch). */
+int fr_has_match_batch(fr_ctx* ctx, const fr_ct* content, size_t n_chars, size_t n_matches, const char* pattern,
+                       fr_ct* out, fr_match_stats* stats);
+/* Plan cache: has_match circuits are data-oblivious, so the lowered, compiled
+ * plan of (pattern, grammar, engine, lowering, multi-value, n_chars, batch size,
+ * start range, content shape) is kept -- its intermediate slots and its
+ * device-resident gate batches -- and a repeat call binds the call's content
+ * slots (a content map read by the keyswitch) and enqueues the levels.  The
+ * content shape is which blocks are trivial (and their values) and which
+ * positions share a ciphertext, not the ciphertexts: fresh content of the same
+ * shape hits.  capacity = plans kept (LRU; default 8, env FR_PLAN_CACHE); 0
+ * disables and frees every cached plan.  max_slots bounds the intermediate arena
+ * slots all cached plans hold ((kN+1) u64 each; default 2^18, env
+ * FR_PLAN_CACHE_SLOTS); eviction runs before a new plan allocates, and a plan
+ * larger than max_slots runs uncached. */
+int fr_set_plan_cache(fr_ctx* ctx, size_t capacity);
+int fr_set_plan_cache_slots(fr_ctx* ctx, size_t max_slots);
+int fr_plan_cache_stats(fr_ctx* ctx, uint64_t* entries, uint64_t* slots, uint64_t* hits, uint64_t* misses);
 
 /* Booleans (block 0 of each handle) to / from a device buffer of n * (kN+1) u64
  * (the start-offset shards' partial results gathered over RCCL without a host
@@ -212,6 +229,9 @@ int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct*
 /* Accumulated kernel timers of the profiling mode (fr_set_profiling): blind
  * rotation and keyswitch milliseconds, launches and bootstraps. */
 int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates);
+/* The part of those blind-rotation timers spent in latency-shape launches (at
+ * most one bootstrap per CU: one workgroup per CU). */
+int fr_device_timers_latency(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, uint64_t* br_gates);
 
 /* ----- one match split across ranks ----- */
 /* The reference folds ct_or over the branches of every start offset
@@ -225,7 +245,12 @@ int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_lau
  * an all-gather imports the other ranks' slices; the last level's output then
  * exists on the ranks that hold it (fr_shard_finish).  Levels are 0-based.
  * export / import synchronise the library's stream before returning; the
- * caller orders its own stream (the all-gather) around them. */
+ * caller orders its own stream (the all-gather) around them.  The plan reads the
+ * content handles' arena slots as they were at fr_shard_plan: the content must
+ * stay alive (not fr_release'd) until fr_shard_free.  fr_shard_plan merges
+ * same-input gates by arena slot, so its levels equal fr_schedule_match's only
+ * when every content handle is distinct and encrypted (fheregex.closure_parts
+ * checks that the two agree). */
 typedef struct fr_shard fr_shard;
 int fr_shard_plan(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
                   size_t start_hi, fr_shard** out, fr_match_stats* stats);

@@ -235,3 +235,15 @@ def test_config5_merged_engine():
 def test_auto_engine_keeps_reference_counts_when_enumerable():
     a = F.plain_match("x" * 64, "/abc/", engine=F.ENGINE_AUTO)
     assert (a.ct_ops, a.cache_hits) == (371, 0)
+
+
+def test_fuzz_scale_lowering_vs_oracle():
+    """The product's engine + lowering (plaintext semantics, fr_plain_match) on the
+    fuzz-at-scale fixture (64-300 chars; tests/golden/make_fuzz_scale.py) against
+    the oracle's position-set simulator results."""
+    with open(os.path.join(GOLDEN, "fuzz_scale.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == 20
+    for c in cases:
+        pm = F.plain_match(c["content"].encode(), c["pattern"], engine=F.ENGINE_AUTO)
+        assert pm.result_lowered == pm.result_recorded == c["expected"], c["pattern"]

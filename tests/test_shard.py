@@ -374,3 +374,70 @@ def test_closure_two_ranks_gpu(key_blob, content, pattern):
     assert np.array_equal(got, ctxs[0].download_radix(ref))  # bit-identical to the unsharded match
     for P in plans:
         P.free()
+
+
+# ----------------------------------------------- full-size sharded parity (GPU)
+def _config4(planted):
+    """BASELINE config 4 content: 1024 letters/spaces without any case variant of
+    'the', planted once at 700 (bench.py make_content 'letters')"""
+    rng = np.random.default_rng(5)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
+    s = bytearray(rng.choice(alpha, 1024))
+    for i in range(len(s) - 2):
+        if bytes(s[i:i + 3]).lower() == b"the":
+            s[i + 2] = ord("x")
+    if planted:
+        s[700:703] = b"ThE"
+    return s.decode()
+
+
+def _config5(bad):
+    import random
+    r5 = random.Random(5)
+    c = "aaa" + "".join(r5.choice(["bc", "de"]) for _ in range(254)) + "f"
+    return c[:300] + "x" + c[301:] if bad else c
+
+
+@pytest.fixture(scope="module")
+def four_ctx(key_blob):
+    """four contexts on device 0 standing in for four ranks"""
+    ctxs = []
+    for _ in range(4):
+        ctx = F.Context(device=0)
+        ctx.load_client_key(key_blob)
+        ctx.gen_server_key(SEED)
+        ctxs.append(ctx)
+    return ctxs
+
+
+FULL = [("config4-planted", "/the/i", lambda: _config4(True)), ("config4-absent", "/the/i", lambda: _config4(False)),
+        ("config5", CONFIG5, lambda: _config5(False)), ("config5-bad", CONFIG5, lambda: _config5(True))]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["closure", "level"])
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("name,pattern,make", FULL, ids=[f[0] for f in FULL])
+def test_full_size_sharded_gpu(four_ctx, name, pattern, make, world, mode):
+    """BASELINE configs 4 (/the/i, 1024 chars, planted and absent) and 5 (512 chars,
+    merged engine) at their full sizes, split over 2 and 4 'ranks' (contexts on
+    device 0) by closure and by level sharding (start offsets engine.rs:15-18,
+    anchors engine.rs:51-57): the result is bit-identical to the unsharded
+    fr_has_match and decrypts to the oracle's position-set simulator bit."""
+    content = make()
+    ctxs = four_ctx[:world]
+    if mode == "closure":
+        plans, out, st = _two_rank_closure(ctxs, content, pattern, seed=31)
+    else:
+        plans, out, st = _two_rank_sharded(ctxs, content, pattern, seed=31)
+    got = ctxs[0].download_radix(out)
+    exp = ro.has_match_reach(content, pattern)
+    assert ctxs[0].decrypt_radix(got) == exp
+    hs = ctxs[0].upload_radix(ctxs[0].encrypt_str(content, seed=31))
+    ref, rst = ctxs[0].has_match(hs, pattern)
+    assert np.array_equal(got, ctxs[0].download_radix(ref))  # bit-identical to the unsharded match
+    assert (st.blind_rotations, st.levels) == (rst.blind_rotations, rst.levels)
+    for P in plans:
+        P.free()
+    for h in hs + [ref, out]:
+        ctxs[0].release(h)

@@ -6,6 +6,6 @@ cd "$(dirname "$0")/.."
 rounds=$1; shift
 for r in $(seq "$rounds"); do
   for lib in "$@"; do
-    FHEREGEX_LIB=$lib timeout -k 10 120 python3 tools/lat_probe.py 7 || exit 1
+    FHEREGEX_LIB=$lib timeout -k 10 120 python3 tools/lat_probe.py 7 ${SIZES:-} || exit 1
   done
 done
