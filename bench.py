@@ -254,7 +254,8 @@ def main():
     ap.add_argument("--ring", default="auto", choices=["auto", "fft", "rns"])
     ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"])
     ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
-    ap.add_argument("--cpu-sample", type=int, default=384, help="gates in the CPU baseline sample (0: skip)")
+    ap.add_argument("--cpu-sample", type=int, default=2048,
+                    help="gates in the CPU baseline sample (0: skip; 2048 ~ 10 s on 16 threads)")
     ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated throughput probe (0: skip)")
     ap.add_argument("--fresh-steps", type=int, default=5,

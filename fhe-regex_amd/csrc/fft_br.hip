@@ -164,11 +164,18 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 // transforms only where it first reads them -- after its own-row products -- so the
 // polynomials need not run in step and one's exchanges can drain while another
 // computes.  FR_POLY_SKEW: s_sleep(1) units by which polynomial P > 0 starts later.
+// FR_POLY_SYNC = 2: workgroup barriers for the exchanges, the late MAC wait only.
+// Measured (tools/ab_libs.sh, profiles/r03/ab_poly_sync.log): one bootstrap 1.337 ms with
+// workgroup barriers, 1.487 ms with FR_POLY_SYNC = 1 at any skew: the software arrivals
+// and polls cost more than the overlap they allow, so the default stays 0.
 #ifndef FR_POLY_SYNC
-#define FR_POLY_SYNC 1
+#define FR_POLY_SYNC 0
 #endif
 #ifndef FR_POLY_SKEW
 #define FR_POLY_SKEW 0
+#endif
+#ifndef FR_POLY_SLEEP
+#define FR_POLY_SLEEP 1
 #endif
 
 template <int M, int E>
@@ -571,7 +578,7 @@ __device__ __forceinline__ void lds_arrive(int* c) {
 __device__ __forceinline__ void lds_wait_ge(int* c, int target) {
     for (int it = 0; it < (1 << 24); ++it) {
         if (__hip_atomic_load((lds_int*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-        __builtin_amdgcn_s_sleep(1);
+        if (FR_POLY_SLEEP) __builtin_amdgcn_s_sleep(1);
     }
     asm volatile("" ::: "memory");
 }
@@ -713,7 +720,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // polynomial's cross-wave exchanges), [4 + P] (its transform written for the MAC),
     // [8 + P] (its MAC reads of the other rows done); WP waves per polynomial; ep =
     // executed steps so far, xg = the polynomial's exchange barriers so far (uniform)
-    constexpr bool PS = LAT && FR_POLY_SYNC;
+    constexpr bool PS = LAT && FR_POLY_SYNC == 1;       // per-polynomial exchange barriers
+    constexpr bool PSM = LAT && FR_POLY_SYNC != 0;      // late MAC wait
     constexpr int WP = T / 64;
     int ep = 0, xg = 0;
     auto poly_sync = [&]() {
@@ -814,7 +822,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         double2 Bc[3][K + 1];
         if constexpr (PRE0) load_slot<M, T, K>(Bc, rs, sbase, P, 0, lane_off);
 #ifndef FR_FFT_NOMACX
-        if constexpr (PS) lds_arrive(pcnt + 4 + P);
+        if constexpr (PSM) lds_arrive(pcnt + 4 + P);
         else __syncthreads();
 #endif
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
@@ -825,7 +833,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // latency shape: computed at the top of the step (the lookups' LDS latency hides
         // behind the digits and the forward FFT); throughput shapes: here (VGPR budget)
         if constexpr (!LAT) psi_factors();
-        if constexpr (PS) {
+        if constexpr (PSM) {
             // own-row products first (they need only this polynomial's transform), then
             // wait for the other polynomials' transforms, then their products: the same
             // operations in the same order per slot as below
@@ -871,7 +879,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 }
                 x[m] = make_double2(zr[m], zi[m]);
             }
-            lds_arrive(pcnt + 8 + P);
+            if constexpr (PS) lds_arrive(pcnt + 8 + P);
         } else
 #pragma unroll
         for (int m = 0; m < E; ++m) {

@@ -409,19 +409,39 @@ def test_plan_cache_replays_bit_identical(gctx):
         gctx.release(h)
 
 
-def _cold(gctx, hs, pattern):
-    """has_match with the plan cache off (a plan compiled for these very slots)"""
-    gctx.set_plan_cache(0)
-    try:
-        o, st = gctx.has_match(hs, pattern)
-    finally:
-        gctx.set_plan_cache(8)
-    w = gctx.download_radix(o)
-    gctx.release(o)
+@pytest.fixture(scope="module")
+def cold_ctx(gctx, key_blob):
+    """A second context with the same keys (same server-key seed) and the plan cache
+    off: the cold reference a cached plan must match bit for bit."""
+    p = gctx.params
+    ctx = F.Context(device=0, params=F.default_params(k=p.k, N=p.N, ring=p.ring))
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    ctx.set_plan_cache(0)
+    return ctx
+
+
+def _cold(gctx, cold, hs, pattern):
+    """has_match in the cold context on the same ciphertext words (trivial handles stay
+    trivial, a handle used twice maps to one handle): the plan compiled for these very
+    slots, no cache involved"""
+    mapped, seen = [], {}
+    for h in hs:
+        if h not in seen:
+            w = gctx.download_radix(h)
+            if not w[:, :-1].any():  # zero masks: a trivial radix (body m * 2^59 per block)
+                seen[h] = cold.trivial(sum(int(w[b, -1] >> np.uint64(59)) << (2 * b) for b in range(4)))
+            else:
+                seen[h] = cold.upload_radix(w)[0]
+        mapped.append(seen[h])
+    o, st = cold.has_match(mapped, pattern)
+    w = cold.download_radix(o)
+    for h in set(seen.values()) | {o}:
+        cold.release(h)
     return w, st
 
 
-def test_plan_cache_fresh_content_hits(gctx):
+def test_plan_cache_fresh_content_hits(gctx, cold_ctx):
     """The plan is keyed on the content's shape, not its slots (engine.rs:8-42
     re-plans every call; the circuit depends only on pattern and length): freshly
     encrypted content of the same length hits the cached plan, and its result is
@@ -437,7 +457,7 @@ def test_plan_cache_fresh_content_hits(gctx):
         o, st = gctx.has_match(hs, "/abc/")
         assert st.plan_cached == (0 if first is None else 1), i
         w = gctx.download_radix(o)
-        cold, st_c = _cold(gctx, hs, "/abc/")
+        cold, st_c = _cold(gctx, cold_ctx, hs, "/abc/")
         assert np.array_equal(w, cold), i
         assert gctx.decrypt_radix(w) == ro.has_match(t, "/abc/").result
         assert (st.pbs, st.blind_rotations, st.levels) == (st_c.pbs, st_c.blind_rotations, st_c.levels)
@@ -446,7 +466,7 @@ def test_plan_cache_fresh_content_hits(gctx):
             gctx.release(h)
 
 
-def test_plan_cache_released_slots_reused(gctx):
+def test_plan_cache_released_slots_reused(gctx, cold_ctx):
     """Content released and new content uploaded into the same arena slots: the
     cache hit reads the new ciphertexts (the content map is bound per call)."""
     s1, s2 = "zzabczzzz", "zzzzzzzzz"
@@ -458,12 +478,12 @@ def test_plan_cache_released_slots_reused(gctx):
     hs2 = gctx.upload_radix(gctx.encrypt_str(s2, seed=41))
     o2, st2 = gctx.has_match(hs2, "/abc/")
     assert st2.plan_cached == 1 and gctx.decrypt_radix(gctx.download_radix(o2)) == 0
-    assert np.array_equal(gctx.download_radix(o2), _cold(gctx, hs2, "/abc/")[0])
+    assert np.array_equal(gctx.download_radix(o2), _cold(gctx, cold_ctx, hs2, "/abc/")[0])
     for h in hs2 + [o2]:
         gctx.release(h)
 
 
-def test_plan_cache_content_shape(gctx):
+def test_plan_cache_content_shape(gctx, cold_ctx):
     """Other shapes miss: a trivial character where the cached plan had a
     ciphertext, and one ciphertext at two positions (merged by the executor);
     each result is bit-identical to its cold plan."""
@@ -476,7 +496,7 @@ def test_plan_cache_content_shape(gctx):
         o2, st2 = gctx.has_match(sh, "/abc/")
         assert st2.plan_cached == 0
         w = gctx.download_radix(o2)
-        assert np.array_equal(w, _cold(gctx, sh, "/abc/")[0])
+        assert np.array_equal(w, _cold(gctx, cold_ctx, sh, "/abc/")[0])
         assert gctx.decrypt_radix(w) == 1
         o3, st3 = gctx.has_match(sh, "/abc/")
         assert st3.plan_cached == 1 and np.array_equal(gctx.download_radix(o3), w)
@@ -486,11 +506,11 @@ def test_plan_cache_content_shape(gctx):
         gctx.release(h)
 
 
-def test_plan_cache_slot_budget(gctx):
+def test_plan_cache_slot_budget(gctx, cold_ctx):
     """A plan larger than the slot budget runs uncached (same bits); the budget
     evicts before allocating and the held slots never exceed it."""
     hs = gctx.upload_radix(gctx.encrypt_str("qqabcq" * 6, seed=60))
-    ref, _ = _cold(gctx, hs, "/abc/")
+    ref, _ = _cold(gctx, cold_ctx, hs, "/abc/")
     gctx.set_plan_cache_slots(10)
     try:
         o, st = gctx.has_match(hs, "/abc/")
@@ -507,7 +527,7 @@ def test_plan_cache_slot_budget(gctx):
 
 
 @pytest.mark.parametrize("pattern", ["/abc/", "/^a{2,8}(bc|de)+[^xyz]$/"])
-def test_has_match_batch_bit_identical(gctx, pattern):
+def test_has_match_batch_bit_identical(gctx, cold_ctx, pattern):
     """fr_has_match_batch: M matches of one pattern in shared launches, each output
     bit-identical to fr_has_match on its own content (cold plan), levels unchanged,
     rotations M times one match's; a repeat with fresh content hits the plan."""
@@ -519,11 +539,11 @@ def test_has_match_batch_bit_identical(gctx, pattern):
         texts = ["aaabcdebcf", "aaabcdebcx", "aadebcbcdf"]
     hss = [gctx.upload_radix(gctx.encrypt_str(t, seed=71 + i)) for i, t in enumerate(texts)]
     outs, st = gctx.has_match_batch(hss, pattern)
-    _, st1 = _cold(gctx, hss[0], pattern)
+    _, st1 = _cold(gctx, cold_ctx, hss[0], pattern)
     assert st.blind_rotations == len(texts) * st1.blind_rotations and st.levels == st1.levels
     for t, hs, o in zip(texts, hss, outs):
         w = gctx.download_radix(o)
-        assert np.array_equal(w, _cold(gctx, hs, pattern)[0]), t
+        assert np.array_equal(w, _cold(gctx, cold_ctx, hs, pattern)[0]), t
         assert gctx.decrypt_radix(w) == ro.has_match_reach(t, pattern)
         gctx.release(o)
     hss2 = [gctx.upload_radix(gctx.encrypt_str(t, seed=90 + i)) for i, t in enumerate(texts)]
