@@ -53,7 +53,7 @@ class Device {
 
     // keys: KSK torus 2^64 [i][j][t]; BSK coefficient domain mod Q [i][r][c][coef]
     void upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk);
-    bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk4_); }
+    bool has_keys() const { return d_ksk_ && (d_bsk_ || d_fbsk_[0]); }
     // server-key generation on the device (keygen.hip; FFT ring): the same keys
     // as gen_ksk + gen_bsk on the host, bit for bit; the torus keys stay on the
     // device for download_server_key
@@ -159,10 +159,13 @@ class Device {
     uint32_t* d_tw_ = nullptr;   // Montgomery zeta per prime [2][N]
     // FR_RING_FFT: Fourier BSK [w][r][c][m][lane] (complex f64, scaled by 1/M), twiddles,
     // psi quadrant table, leaf exponents (fft.h)
-    int fft_e_ = 4;           // complex points per lane in the throughput shape (4 or 8; 4 measured faster)
+    int fft_e_ = 4;           // complex points per lane in the throughput shape (4, 8 or 16)
     size_t fft_small_ = 256;  // launches of at most this many bootstraps use the latency shape
-    double* d_fbsk_ = nullptr;  // layout for E = 8 (k = 2 only)
-    double* d_fbsk4_ = nullptr;  // layout for E = 4
+    // Fourier BSK, one copy per lane geometry in use: [0] E = 4 (latency shape, always),
+    // [1] E = 8, [2] E = 16 (the throughput shape's when fft_e_ is that)
+    double* d_fbsk_[3] = {nullptr, nullptr, nullptr};
+    static int fbsk_index(int E) { return E == 4 ? 0 : E == 8 ? 1 : 2; }
+    bool fbsk_needed(int E) const { return E == 4 || E == fft_e_; }
     double* d_ftw_ = nullptr;
     double* d_fqt_ = nullptr;   // psi^k, k < 2N
     uint16_t* d_fleaf_ = nullptr;

@@ -1014,7 +1014,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 // ================================================================== host side
 // compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
 // BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
-// k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4)
+// k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4).  E = 8 and 16
+// (two waves / one wave per polynomial) were measured slower at every batch size
+// (profiles/r03/ab_lane_elems_k1.log) and would need a radix-4 inverse to stay bit-exact.
 template <int N, int K, int E>
 constexpr bool fft_shape_ok() {
     return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
@@ -1072,8 +1074,11 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
     // slot order -> per-lane order [poly][m][lane] (one copy per lane geometry E):
     // lane tl's element m is slot idx<LAST>(tl, m), so each load of a wave is 1 KB contiguous
     std::vector<fft::c64> lanes(four.size());
-    for (int E : {8, 4}) {
-        if (!fft_supported(p_.k, N, E)) continue;
+    for (int E : {16, 8, 4}) {
+        double*& dst = d_fbsk_[fbsk_index(E)];
+        (void)hipFree(dst);
+        dst = nullptr;
+        if (!fft_supported(p_.k, N, E) || !fbsk_needed(E)) continue;
         const int T = M / E;
         int e = 0;
         while ((1 << e) < E) ++e;
@@ -1084,9 +1089,6 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
             for (int m = 0; m < E; ++m) slot[(size_t)m * T + tl] = geo_base(tabs.LOG, e, LAST, tl, V) + (m << L);
         for (size_t pq = 0; pq < polys; ++pq)
             for (size_t q = 0; q < (size_t)M; ++q) lanes[pq * M + q] = four[pq * M + slot[q]];
-        double*& dst = E == 8 ? d_fbsk_ : d_fbsk4_;
-        (void)hipFree(dst);
-        dst = nullptr;
         FFT_CHECK(hipMalloc(&dst, 16 * lanes.size()));
         FFT_CHECK(hipMemcpy(dst, lanes.data(), 16 * lanes.size(), hipMemcpyHostToDevice));
     }
@@ -1101,7 +1103,7 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
             constexpr bool LAT = decltype(lat)::value;
             if constexpr (fft_shape_ok<N, K, E>())
             k_blind_rotate_fft<N, K, E, LAT><<<(unsigned)n, fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT>(), s>>>(
-                d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)(E == 8 ? d_fbsk_ : d_fbsk4_),
+                d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)d_fbsk_[fbsk_index(E)],
                 (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
         };
         using I4 = std::integral_constant<int, 4>;
@@ -1115,12 +1117,13 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
 }
 
 void Device::free_fft() {
-    (void)hipFree(d_fbsk_);
-    (void)hipFree(d_fbsk4_);
+    for (auto& b : d_fbsk_) {
+        (void)hipFree(b);
+        b = nullptr;
+    }
     (void)hipFree(d_ftw_);
     (void)hipFree(d_fqt_);
     (void)hipFree(d_fleaf_);
-    d_fbsk_ = d_fbsk4_ = nullptr;
     d_ftw_ = d_fqt_ = nullptr;
     d_fleaf_ = nullptr;
 }

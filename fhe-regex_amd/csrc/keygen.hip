@@ -135,12 +135,19 @@ __global__ void __launch_bounds__(256) k_gen_bsk(uint64_t seed, int k, const uin
     }
 }
 
+// element m of lane tl in the last-phase layout of lane geometry E (slot order, geo.h)
+template <int M, int E>
+__device__ __forceinline__ int lane_slot(int tl, int m) {
+    constexpr int LOG = __builtin_ctz(M), e = __builtin_ctz(E), LAST = (LOG + e - 1) / e - 1;
+    return geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << geo_lo(LOG, e, LAST));
+}
 // fold + forward FFT + 1/M of one polynomial, written in the lane layouts of
-// the E = 8 and E = 4 kernels ([poly][m][lane], slot of (lane, m) per geo.h)
+// the E = 4, 8 and 16 kernels ([poly][m][lane], slot of (lane, m) per geo.h; a null
+// output is skipped)
 template <int N>
 __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict__ bsk, const double2* __restrict__ tw,
-                                                     int L8, int L4, double2* __restrict__ out8,
-                                                     double2* __restrict__ out4) {
+                                                     double2* __restrict__ out4, double2* __restrict__ out8,
+                                                     double2* __restrict__ out16) {
     constexpr int M = N / 2;
     constexpr int LOG = __builtin_ctz(M);
     __shared__ double2 z[M];
@@ -163,19 +170,17 @@ __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict_
     }
     const double scale = 1.0 / (double)M;  // 2^-LOG, exact
     for (int idx = tid; idx < M; idx += 256) {
-        if (out8) {  // E = 8 (k = 2 only)
-            constexpr int E = 8, e = 3, T = M / E, LAST = (LOG + e - 1) / e - 1;
-            const int m = idx / T, tl = idx % T;
-            const int slot = geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << L8);
-            const double2 v = z[slot];
+        if (out4) {
+            const double2 v = z[lane_slot<M, 4>(idx % (M / 4), idx / (M / 4))];
+            out4[p * M + idx] = make_double2(v.x * scale, v.y * scale);
+        }
+        if (out8) {
+            const double2 v = z[lane_slot<M, 8>(idx % (M / 8), idx / (M / 8))];
             out8[p * M + idx] = make_double2(v.x * scale, v.y * scale);
         }
-        {  // E = 4
-            constexpr int E = 4, e = 2, T = M / E, LAST = (LOG + e - 1) / e - 1;
-            const int m = idx / T, tl = idx % T;
-            const int slot = geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << L4);
-            const double2 v = z[slot];
-            out4[p * M + idx] = make_double2(v.x * scale, v.y * scale);
+        if (out16) {
+            const double2 v = z[lane_slot<M, 16>(idx % (M / 16), idx / (M / 16))];
+            out16[p * M + idx] = make_double2(v.x * scale, v.y * scale);
         }
     }
 }
@@ -302,20 +307,18 @@ void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
         else k_gen_bsk<1024><<<(unsigned)(nw * kp1), 256, 0, s>>>(seed, p_.k, d_sb, d_msg, d_bn, gadget, d_tbsk_);
         KG_CHECK(hipGetLastError());
 
-        // Fourier BSK in the lane layouts of the shapes (E = 4; k = 2 also E = 8)
-        for (double** dst : {&d_fbsk_, &d_fbsk4_}) {
-            (void)hipFree(*dst);
-            *dst = nullptr;
-            if (dst == &d_fbsk4_ || p_.k == 2) KG_CHECK(hipMalloc(dst, 16 * bsk_polys * M));
+        // Fourier BSK in the lane layouts of the shapes in use (E = 4, and the throughput shape's)
+        for (int E : {4, 8, 16}) {
+            double*& dst = d_fbsk_[fbsk_index(E)];
+            (void)hipFree(dst);
+            dst = nullptr;
+            if (fbsk_needed(E) && (E < 16 || p_.k == 1)) KG_CHECK(hipMalloc(&dst, 16 * bsk_polys * M));
         }
-        const int LOG = __builtin_ctz(M);
-        const int L8 = geo_lo(LOG, 3, (LOG + 2) / 3 - 1), L4 = geo_lo(LOG, 2, (LOG + 1) / 2 - 1);
+        double2 *o4 = (double2*)d_fbsk_[0], *o8 = (double2*)d_fbsk_[1], *o16 = (double2*)d_fbsk_[2];
         if (N == 2048)
-            k_bsk_fourier<2048><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
-                                                                    (double2*)d_fbsk_, (double2*)d_fbsk4_);
+            k_bsk_fourier<2048><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, o4, o8, o16);
         else
-            k_bsk_fourier<1024><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, L8, L4,
-                                                                    (double2*)d_fbsk_, (double2*)d_fbsk4_);
+            k_bsk_fourier<1024><<<(unsigned)bsk_polys, 256, 0, s>>>(d_tbsk_, (const double2*)d_ftw_, o4, o8, o16);
         KG_CHECK(hipGetLastError());
         KG_CHECK(hipStreamSynchronize(s));
     } catch (...) {

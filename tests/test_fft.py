@@ -263,3 +263,23 @@ def test_fft_metric_config_256_chars(fctx):
     hs2 = fctx.upload_radix(fctx.encrypt_str(s2, seed=10))
     out2, _ = fctx.has_match(hs2, "/abc/")
     assert fctx.decrypt_radix(fctx.download_radix(out2)) == ro.has_match(s2, "/abc/").result
+
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("keygen", [F.KEYGEN_AUTO, F.KEYGEN_HOST])
+def test_fft_throughput_shape_bit_exact(key_blob, oracle_fft, point, keygen):
+    """The throughput shape on a batch large enough for it (300 > the latency shape's
+    256), with the Fourier key laid out by the device keygen and by the host upload:
+    bit-exact against the oracle."""
+    ctx = F.Context(device=0, params=F.default_params(k=point[0], N=point[1], ring=F.RING_FFT))
+    ctx.load_client_key(key_blob)
+    ctx.set_keygen(keygen)
+    ctx.gen_server_key(SEED)
+    O = oracle_fft
+    rng = np.random.default_rng(300)
+    ks = rng.integers(0, 2**64 - 1, (300, O.n + 1), dtype=np.uint64, endpoint=True)
+    luts = [[(5 * m + i) % 16 for m in range(16)] for i in range(300)]
+    got = ctx.dev_blind_rotate(ks, luts)
+    for i in (0, 1, 150, 299):
+        assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i

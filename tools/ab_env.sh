@@ -8,6 +8,6 @@ for r in $(seq "$rounds"); do
   for e in "$@"; do
     if [ "$e" = "-" ]; then e=""; fi
     echo -n "[$e] "
-    env $e timeout -k 10 120 python3 tools/lat_probe.py 7 || exit 1
+    env $e timeout -k 10 120 python3 tools/lat_probe.py 7 ${SIZES:-} || exit 1
   done
 done
