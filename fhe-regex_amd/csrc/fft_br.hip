@@ -158,25 +158,15 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_LAT_TWR
 #define FR_LAT_TWR 1
 #endif
-// latency shape: per-polynomial synchronisation (1) instead of workgroup barriers (0).
-// The cross-wave exchanges of a polynomial's transforms wait for that polynomial's own
-// waves only (LDS arrival counters), and the MAC waits for the other polynomials'
-// transforms only where it first reads them -- after its own-row products -- so the
-// polynomials need not run in step and one's exchanges can drain while another
-// computes.  FR_POLY_SKEW: s_sleep(1) units by which polynomial P > 0 starts later.
-// FR_POLY_SYNC = 2: workgroup barriers for the exchanges, the late MAC wait only.
-// Measured (tools/ab_libs.sh, profiles/r03/ab_poly_sync.log): one bootstrap 1.337 ms with
-// workgroup barriers, 1.487 ms with FR_POLY_SYNC = 1 at any skew: the software arrivals
-// and polls cost more than the overlap they allow, so the default stays 0.
-#ifndef FR_POLY_SYNC
-#define FR_POLY_SYNC 0
-#endif
-#ifndef FR_POLY_SKEW
-#define FR_POLY_SKEW 0
-#endif
-#ifndef FR_POLY_SLEEP
-#define FR_POLY_SLEEP 1
-#endif
+// Round-3 latency-shape experiments, measured and not kept (logs under profiles/r03/):
+//  * per-polynomial synchronisation: LDS arrival counters in place of the workgroup
+//    barriers around each polynomial's cross-wave exchanges, and the MAC waiting for the
+//    other polynomial only where it reads it: 1.49 against 1.34 ms per bootstrap, at any
+//    start skew; the late MAC wait alone: 1.35 (ab_poly_sync.log);
+//  * the MAC's key products computed in the shadow of the forward cross-wave exchange,
+//    the next step's key loaded right after them: 1.38 ms (ab_kearly.log);
+//  * k = 1 throughput shapes with E = 8 / 16 (two waves / one wave per polynomial): 12.0 /
+//    13.4 against 10.8 ms per 2048 bootstraps (ab_lane_elems_k1.log).
 
 template <int M, int E>
 constexpr int ftw_index(int s, int m) {
@@ -350,13 +340,8 @@ constexpr bool fxkeep_ok() {
     }
     return true;
 }
-// the barrier of a cross-wave exchange: the workgroup's, or (latency shape with
-// FR_POLY_SYNC) the polynomial's own four waves (poly_sync below)
-struct WgSync {
-    __device__ __forceinline__ void operator()() const { __syncthreads(); }
-};
-template <int M, int E, int PF, int PT, bool PRE, bool XK = false, class Sync = WgSync>
-__device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl, Sync&& sync = Sync{}) {
+template <int M, int E, int PF, int PT, bool PRE, bool XK = false>
+__device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
     using G = FGeo<M, E>;
     if constexpr (fperm_ok<M, E, PF, PT>()) {
         // a pre-barrier would also order the next exchange's writes: keep the plan's barriers
@@ -381,7 +366,7 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl,
 #pragma unroll
             for (int m = 0; m < E; ++m)
                 if (m != q) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
-            sync();
+            __syncthreads();
 #pragma unroll
             for (int m = 0; m < E; ++m)
                 if (m != q) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
@@ -390,7 +375,7 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl,
 #pragma unroll
         for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
         if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
-        else sync();
+        else __syncthreads();
 #pragma unroll
         for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
     }
@@ -425,27 +410,27 @@ constexpr bool fexchanges_conflict_free() {
 // hook(integral_constant<p>) runs after phase p's butterflies (before its exchange).
 // CARRY: a pre-barrier owed by a register exchange (which writes no LDS) moves to the
 // next LDS exchange's write.
-template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false, class Hook, class Sync = WgSync>
+template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false, class Hook>
 __device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
-                                              const double2* tw, int tl, Hook&& hook, Sync&& sync = Sync{}) {
+                                              const double2* tw, int tl, Hook&& hook) {
     if constexpr (TWR) ffwd_phase_r<M, E, p>(x, twr);
     else ffwd_phase<M, E, p>(x, tw, tl);
     hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
         constexpr bool pre = !NOPRE && (ffwd_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p + 1>();
-        fexchange<M, E, p, p + 1, reg ? false : pre, !NOPRE>(x, row, tl, sync);
-        fforward_from<M, E, p + 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl, hook, sync);
+        fexchange<M, E, p, p + 1, reg ? false : pre, !NOPRE>(x, row, tl);
+        fforward_from<M, E, p + 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl, hook);
     }
 }
-template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false, class Sync = WgSync>
+template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false>
 __device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
-                                              const double2* tw, const double2* twc, int tl, Sync&& sync = Sync{}) {
+                                              const double2* tw, const double2* twc, int tl) {
     if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
     else finv_phase_lds<M, E, p>(x, tw, twc, tl);
     if constexpr (p > 0) {
         constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
-        fexchange<M, E, p, p - 1, reg ? false : pre, !NOPRE>(x, row, tl, sync);
-        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, twc, tl, sync);
+        fexchange<M, E, p, p - 1, reg ? false : pre, !NOPRE>(x, row, tl);
+        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, twc, tl);
     }
 }
 
@@ -489,7 +474,7 @@ template <int N, int K, int E, bool LAT>
 constexpr size_t fbr_smem_bytes() {
     return 16 * ((LAT ? 2 : 1) * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 +
                  (LAT ? (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
-           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT + 2 * 514 + 4 * 12;
+           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT + 2 * 514;
 }
 // workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
 template <int K, int E>
@@ -565,24 +550,6 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
     return acc;
 }
 
-// LDS arrival counters of the per-polynomial synchronisation: a wave arrives after its
-// LDS writes completed (lgkmcnt(0); no vmcnt wait, so in-flight key loads survive) and
-// polls the counter from LDS with s_sleep.  The poll is bounded so that a logic error
-// could not hang the GPU (every wave of the workgroup runs the same arrivals, so the
-// bound is never reached).
-typedef __attribute__((address_space(3))) int lds_int;
-__device__ __forceinline__ void lds_arrive(int* c) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add((lds_int*)c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-__device__ __forceinline__ void lds_wait_ge(int* c, int target) {
-    for (int it = 0; it < (1 << 24); ++it) {
-        if (__hip_atomic_load((lds_int*)c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= target) break;
-        if (FR_POLY_SLEEP) __builtin_amdgcn_s_sleep(1);
-    }
-    asm volatile("" ::: "memory");
-}
-
 template <int N, int K, int E, bool LAT>
 __global__ void __launch_bounds__((fbr_threads<N, K, E>()), (fbr_min_waves<N, K, E, LAT>()))
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
@@ -608,7 +575,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
     int* wcnt = (int*)(wterms + 16 * MAX_OUT);
     uint16_t* nxt = (uint16_t*)(wcnt + MAX_OUT);  // (latency shape) next unskipped step >= t, t <= steps
-    int* pcnt = (int*)(nxt + 514);  // (FR_POLY_SYNC) per polynomial: exchange, MAC-written, MAC-read counters
 
     const int tid = threadIdx.x;
     const int P = __builtin_amdgcn_readfirstlane(tid / T), tl = tid % T;  // wave-uniform polynomial
@@ -626,7 +592,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         fft::cmul(c.x, c.y, ca.x, ca.y, twc[i].x, twc[i].y);
     }
     for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
-    if (tid < 12) pcnt[tid] = 0;
     for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
     if (tid == 0) abar[n] = 0;  // pad an odd n
     const uint32_t bbar = mod_switch(in[n], LOG2N2);
@@ -716,30 +681,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         const int t0 = __builtin_amdgcn_readfirstlane((int)nxt[0]);
         for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, t0 < steps ? t0 : 0);
     }
-    // per-polynomial synchronisation (FR_POLY_SYNC, latency shape): counters [P] (the
-    // polynomial's cross-wave exchanges), [4 + P] (its transform written for the MAC),
-    // [8 + P] (its MAC reads of the other rows done); WP waves per polynomial; ep =
-    // executed steps so far, xg = the polynomial's exchange barriers so far (uniform)
-    constexpr bool PS = LAT && FR_POLY_SYNC == 1;       // per-polynomial exchange barriers
-    constexpr bool PSM = LAT && FR_POLY_SYNC != 0;      // late MAC wait
-    constexpr int WP = T / 64;
-    int ep = 0, xg = 0;
-    auto poly_sync = [&]() {
-        lds_arrive(pcnt + P);
-        ++xg;
-        lds_wait_ge(pcnt + P, WP * xg);
-    };
-    if constexpr (PS && FR_POLY_SKEW > 0) {
-        if (P > 0)
-            for (int i = 0; i < FR_POLY_SKEW * P; ++i) __builtin_amdgcn_s_sleep(1);
-    }
     for (int t = 0; t < steps; ++t) {
         if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
         FBR_STAMP(0);
-        if constexpr (PS) {  // the other polynomials have read this row's previous transform
-#pragma unroll
-            for (int q = 0; q < K; ++q) lds_wait_ge(pcnt + 8 + other_row<K>(P, q), WP * ep);
-        }
         // the step's byte offset in the key (uniform: soffset of every load)
         const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
         // groups NPF.. of this step: G_TOP at the top of the step, G_L1 / G_L2 after forward
@@ -786,10 +730,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int m = 0; m < E; ++m) x[m] = make_double2(fft::acc_digit<23>(alo[m]), fft::acc_digit<23>(ahi[m]));
         FBR_STAMP(1);
         // 2. forward FFT (latency shape: GGSW groups 1 and 2 issued at phase boundaries)
-        auto xsync = [&]() {
-            if constexpr (PS) poly_sync();
-            else __syncthreads();
-        };
         fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
             if constexpr (LAT) {
                 constexpr int p = decltype(ph)::value;
@@ -804,7 +744,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                     __builtin_amdgcn_sched_barrier(0);
                 }
             }
-        }, xsync);
+        });
         FBR_STAMP(2);
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #ifndef FR_FFT_NOMACX  // timing experiment only (wrong results): no MAC exchange
@@ -822,8 +762,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         double2 Bc[3][K + 1];
         if constexpr (PRE0) load_slot<M, T, K>(Bc, rs, sbase, P, 0, lane_off);
 #ifndef FR_FFT_NOMACX
-        if constexpr (PSM) lds_arrive(pcnt + 4 + P);
-        else __syncthreads();
+        __syncthreads();
 #endif
         // slot factors psi^(e L) for e = a_i, a_j and their product for a_i + a_j.
         // Slot m of this lane has L = Lb + M s_m: Lb = L mod M is shared by the
@@ -833,54 +772,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // latency shape: computed at the top of the step (the lookups' LDS latency hides
         // behind the digits and the forward FFT); throughput shapes: here (VGPR budget)
         if constexpr (!LAT) psi_factors();
-        if constexpr (PSM) {
-            // own-row products first (they need only this polynomial's transform), then
-            // wait for the other polynomials' transforms, then their products: the same
-            // operations in the same order per slot as below
-            double zr[E], zi[E], kxr[E][K], kxi[E][K];
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-                const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
-                double cr[3], ci[3];
-#pragma unroll
-                for (int h = 1; h < 3; ++h)
-                    fft::psi_quadrant(bre[h - 1][m >> 2], bim[h - 1][m >> 2], ((h == 1 ? ei : ej) * sm) & 3u, cr[h], ci[h]);
-                fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
-                double kor, koi;
-#pragma unroll
-                for (int gg = 0; gg < 3; ++gg) {
-                    const double c1r = cr[gg] - 1.0, c1i = ci[gg];
-                    const double2 Bo = gv[gg][0][LAT ? m : 0];
-                    if (gg == 0) fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
-                    else fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
-#pragma unroll
-                    for (int q = 0; q < K; ++q) {
-                        const double2 Bx = gv[gg][1 + q][LAT ? m : 0];
-                        if (gg == 0) fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr[m][q], kxi[m][q]);
-                        else fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr[m][q], kxi[m][q]);
-                    }
-                }
-                fft::cmul(x[m].x, x[m].y, kor, koi, zr[m], zi[m]);
-            }
-#ifndef FR_FFT_NOMACX
-#pragma unroll
-            for (int q = 0; q < K; ++q) lds_wait_ge(pcnt + 4 + other_row<K>(P, q), WP * (ep + 1));
-#endif
-#pragma unroll
-            for (int m = 0; m < E; ++m) {
-#pragma unroll
-                for (int q = 0; q < K; ++q) {
-#ifdef FR_FFT_NOMACX
-                    const double2 oth = make_double2(x[m].y, x[m].x);
-#else
-                    const double2 oth = orow_bl[q][G::template at<XL>(G::template moff<LAST>(m))];
-#endif
-                    fft::cmac(oth.x, oth.y, kxr[m][q], kxi[m][q], zr[m], zi[m]);
-                }
-                x[m] = make_double2(zr[m], zi[m]);
-            }
-            if constexpr (PS) lds_arrive(pcnt + 8 + P);
-        } else
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             double2 Bn[3][K + 1];
@@ -945,8 +836,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
-        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, twc, tl, xsync);
-        ++ep;
+        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, twc, tl);
         FBR_STAMP(4);
 #pragma unroll
         for (int m = 0; m < E; ++m) {
@@ -1014,9 +904,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 // ================================================================== host side
 // compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
 // BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
-// k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4).  E = 8 and 16
-// (two waves / one wave per polynomial) were measured slower at every batch size
-// (profiles/r03/ab_lane_elems_k1.log) and would need a radix-4 inverse to stay bit-exact.
+// k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4)
 template <int N, int K, int E>
 constexpr bool fft_shape_ok() {
     return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
