@@ -354,6 +354,7 @@ def main():
 
     batch = [encrypt(c, 7 + 1000 * rank + m) for m, c in enumerate(contents)]
     handles = batch[0]
+    handles_np = np.asarray(handles, dtype=np.uint32)  # passed without a per-call ctypes copy
 
     plan = None
     phase = {}
@@ -373,7 +374,7 @@ def main():
         """one step; returns ([result handles] on rank 0 (else []), rotations run by this rank, stats)"""
         if shard == "matches":
             if M == 1:
-                out, st = ctx.has_match(handles, pattern)
+                out, st = ctx.has_match(handles_np, pattern)
                 return [out], st.blind_rotations, st
             outs, st = ctx.has_match_batch(batch, pattern)
             return outs, st.blind_rotations, st
@@ -422,9 +423,12 @@ def main():
 
     first_call = None
     for _ in range(args.warmup):
+        t = time.perf_counter()
         o, _, st0 = step()
-        if first_call is None:  # cold call: parse, record, lower, compile, plan upload
-            first_call = {"host_ms": st0.host_ms, "device_ms": st0.device_ms, "plan_cached": st0.plan_cached}
+        if first_call is None:  # cold call: parse, record, lower, compile, plan upload, and its device time
+            torch.cuda.synchronize()
+            first_call = {"host_ms": st0.host_ms, "wall_ms": (time.perf_counter() - t) * 1e3,
+                          "plan_cached": st0.plan_cached}
         for h in o:
             ctx.release(h)
 
@@ -482,23 +486,25 @@ def main():
 
     fresh = None
     if args.fresh_steps and world == 1 and M == 1:
-        # newly encrypted content every step (device encryption outside the timing): the
-        # template plan is replayed with the new content's slots bound
-        ms, cached, ok = [], [], True
-        for i in range(args.fresh_steps):
-            c = make_content(kind, L, seed=100 + i)
-            hs = ctx.encrypt_upload_str(c, seed=500 + i)
-            torch.cuda.synchronize()
-            t = time.perf_counter()
-            o, stf = ctx.has_match(hs, pattern)
-            ms.append((time.perf_counter() - t) * 1e3)
-            cached.append(stf.plan_cached)
-            exp_f = F.plain_match(c, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
-            ok &= ctx.decrypt_radix(ctx.download_radix(o)) == exp_f
-            for h in hs + [o]:
-                ctx.release(h)
-        fresh = {"fresh_content_ms": float(np.mean(ms)), "ms": ms, "plan_cached": cached, "results_ok": bool(ok),
+        # newly encrypted content for every match (device encryption before the timing): the
+        # template plan is replayed with each content's slots bound; timed like the replay
+        # (back-to-back matches, one synchronise at the end)
+        cs = [make_content(kind, L, seed=100 + i) for i in range(args.fresh_steps)]
+        hss = [np.asarray(ctx.encrypt_upload_str(c, seed=500 + i), dtype=np.uint32) for i, c in enumerate(cs)]
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        res = [ctx.has_match(h, pattern) for h in hss]
+        torch.cuda.synchronize()
+        fresh_ms = (time.perf_counter() - t) * 1e3 / args.fresh_steps
+        ok = all(ctx.decrypt_radix(ctx.download_radix(o)) ==
+                 F.plain_match(c, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+                 for (o, _), c in zip(res, cs))
+        fresh = {"fresh_content_ms": fresh_ms, "matches": args.fresh_steps,
+                 "plan_cached": [int(stf.plan_cached) for _, stf in res], "results_ok": bool(ok),
                  "replay_ms": elapsed / args.steps * 1e3}
+        for (o, _), hs in zip(res, hss):
+            for h in list(hs) + [o]:
+                ctx.release(int(h))
 
     kernel = None
     if args.saturate and rank == 0:
@@ -510,10 +516,10 @@ def main():
                   "br_pbs_per_s": 2 * args.saturate / (br_sat / 1e3)}
 
     probe = None
-    if args.probe and rank == 0:
+    if args.probe.strip("' ") and rank == 0:
         src = [h for h in handles if h != F.NULL_CT]
         probe = {}
-        for cnt in [int(x) for x in args.probe.split(",")]:
+        for cnt in [int(x) for x in args.probe.replace("'", "").split(",") if x.strip("' ")]:
             hs = [src[i % len(src)] for i in range(cnt)]
             ctx.dev_bench_pbs(hs, 1)  # warm-up (the first launch of a shape runs on a cold clock)
             br_p, tot_p = ctx.dev_bench_pbs(hs, 2)

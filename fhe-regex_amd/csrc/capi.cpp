@@ -4,7 +4,6 @@
 #include <climits>
 #include <cstdlib>
 #include <map>
-#include <unordered_map>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -84,7 +83,12 @@ struct fr_ctx {
     int keygen = FR_KEYGEN_AUTO;
     bool sk_on_device = false;  // server key generated on the device (export downloads it)
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
+    bool async_match = true;  // has_match returns once its launches are enqueued (fr_set_async)
     fr_plan_cache* plans = nullptr;
+    // content_signature scratch: canonical id of an arena slot, valid while sig_gen[slot] == gen
+    std::vector<int32_t> sig_id;
+    std::vector<uint32_t> sig_gen;
+    uint32_t gen = 0;
 
     fr_ctx();
     ~fr_ctx();
@@ -431,7 +435,11 @@ static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content,
     std::vector<int32_t> sig;
     sig.reserve(4 * n);
     if (cmap) cmap->assign(4 * n, -1);
-    std::unordered_map<int, int32_t> first;
+    if (++ctx->gen == 0) {  // generation wrapped: forget every stamp
+        std::fill(ctx->sig_gen.begin(), ctx->sig_gen.end(), 0u);
+        ctx->gen = 1;
+    }
+    int32_t next_id = 0;
     for (size_t q = 0; q < n; ++q) {
         if (content[q] == 0xFFFFFFFFu) {
             sig.insert(sig.end(), 4, ABSENT);
@@ -445,8 +453,15 @@ static std::vector<int32_t> content_signature(fr_ctx* ctx, const fr_ct* content,
             } else if (s < 0) {
                 sig.push_back(-1 - (int32_t)h.b[b].triv);
             } else {
-                auto it = first.emplace(s, (int32_t)first.size()).first;
-                sig.push_back(it->second);
+                if ((size_t)s >= ctx->sig_id.size()) {
+                    ctx->sig_id.resize((size_t)s + 1024);
+                    ctx->sig_gen.resize((size_t)s + 1024, 0u);
+                }
+                if (ctx->sig_gen[s] != ctx->gen) {
+                    ctx->sig_gen[s] = ctx->gen;
+                    ctx->sig_id[s] = next_id++;
+                }
+                sig.push_back(ctx->sig_id[s]);
             }
             if (cmap) (*cmap)[4 * q + b] = s;
         }
@@ -537,7 +552,7 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
             const int og = hit->out_gate < 0 ? -1 : hit->out_gate + (int)(m * hit->n_gates);
             outs[m] = make_output(ctx, og, hit->out_w, hit->out_const, hit->plan.slot, false);
         }
-        dev.sync();
+        if (!ctx->async_match) dev.sync();
     } else {
         ++pc.misses;
         ValueDag dag;
@@ -597,9 +612,9 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
             t1 = now_ms();
             launch_plan(dev, P);
             for (size_t m = 0; m < M; ++m) outs[m] = make_output(ctx, out_of(m), prog.out_w, prog.out_const, P.slot, true);
-            free_plan_slots(dev, P.slot);
+            free_plan_slots(dev, P.slot);  // later users of these slots are ordered after the launches (one stream)
         }
-        dev.sync();
+        if (!ctx->async_match) dev.sync();
     }
     double t2 = now_ms();
     if (st) {
@@ -1243,6 +1258,13 @@ int fr_set_plan_cache(fr_ctx* ctx, size_t capacity) {
         NEED(ctx);
         ctx->plans->capacity = capacity;
         evict_for(ctx, 0, 0);  // drop the least recently used beyond the new capacity
+    })
+}
+
+int fr_set_async(fr_ctx* ctx, int32_t on) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->async_match = on != 0;
     })
 }
 

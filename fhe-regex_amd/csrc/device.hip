@@ -1326,6 +1326,8 @@ void Device::bind_content(const int* cmap, size_t n) {
         for (auto& h : h_cmap_) HIP_CHECK(hipHostMalloc(&h, 4 * cap));
         cmap_cap_ = cap;
     }
+    // the map bound last is still in place (a replay of the same content): nothing to copy
+    if (n == cmap_n_ && n && std::memcmp(h_cmap_[cmap_stage_], cmap, 4 * n) == 0) return;
     cmap_stage_ ^= 1;
     // the pinned buffer is rewritten only after its previous copy completed
     HIP_CHECK(hipEventSynchronize((hipEvent_t)cmap_ev_[cmap_stage_]));

@@ -140,6 +140,7 @@ _SIGS = {
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
+    "fr_set_async": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_plan_cache_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "fr_has_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_size_t, C.c_char_p,
@@ -323,6 +324,10 @@ class Context:
         """Plans kept for repeat has_match calls (0: off, frees the cached plans)."""
         _check(lib().fr_set_plan_cache(self.h, capacity))
 
+    def set_async(self, on: bool):
+        """has_match returns once its launches are enqueued (default) or blocks (False)."""
+        _check(lib().fr_set_async(self.h, int(on)))
+
     def set_plan_cache_slots(self, max_slots: int):
         """Bound on the intermediate arena slots held by all cached plans."""
         _check(lib().fr_set_plan_cache_slots(self.h, max_slots))
@@ -441,7 +446,12 @@ class Context:
 
     def has_match(self, content: Sequence[int], pattern: str, start_lo: Optional[int] = None,
                   start_hi: Optional[int] = None):
-        arr = (C.c_uint32 * len(content))(*content)
+        """engine.rs:8-42 over content handles (a sequence, or a uint32 numpy array: no copy)"""
+        if isinstance(content, np.ndarray):
+            content = np.ascontiguousarray(content, dtype=np.uint32)
+            arr = content.ctypes.data_as(C.POINTER(C.c_uint32))
+        else:
+            arr = (C.c_uint32 * len(content))(*content)
         out = C.c_uint32()
         st = MatchStats()
         if start_lo is None and start_hi is None:

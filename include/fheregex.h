@@ -88,7 +88,7 @@ typedef struct {
     uint64_t levels;        /* dependent PBS levels (launch batches) */
     uint64_t max_level_width;
     double host_ms;         /* parse + enumerate + record + lower + compile (plan-cache hit: the lookup) */
-    double device_ms;       /* device execution, wall */
+    double device_ms;       /* device execution, wall (fr_set_async on: until the launches are enqueued) */
     double br_kernel_ms;    /* sum of blind-rotation kernel durations (HIP events) */
     double ks_kernel_ms;    /* sum of lincomb+keyswitch kernel durations (HIP events) */
     uint64_t br_launches;
@@ -189,7 +189,13 @@ int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n);
 /* ----- the engine (engine.rs:8-42) ----- */
 /* Enumerate, record, lower and execute has_match over content handles.  The
  * result is a boolean radix handle (decrypts to 0/1).  Pattern errors return
- * FR_ERR_PARSE / FR_ERR_REF_PANIC like the reference. */
+ * FR_ERR_PARSE / FR_ERR_REF_PANIC like the reference.  By default the call returns
+ * once the match's launches are enqueued on the context's stream: the result
+ * handle can be used at once (every later operation of the context is ordered after
+ * the match, and downloads wait for it), so consecutive matches overlap their host
+ * work with the device's; fr_set_async(ctx, 0) makes the engine calls block until
+ * the device has finished. */
+int fr_set_async(fr_ctx* ctx, int32_t on);
 int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, fr_ct* out,
                  fr_match_stats* stats);
 /* Same, restricted to start offsets [start_lo, start_hi) — the per-GPU shard of

@@ -555,6 +555,36 @@ def test_has_match_batch_bit_identical(gctx, cold_ctx, pattern):
         gctx.release(h)
 
 
+def test_async_matches_chain_and_block(gctx):
+    """has_match returns once its launches are enqueued (default): the result handle
+    feeds further ops at once (NOT, OR), back-to-back matches with released outputs
+    reuse slots in stream order, and the blocking mode (fr_set_async 0) gives the same
+    words."""
+    s1, s2 = "qqabcqqqq", "qqqqqqqqq"
+    h1 = gctx.upload_radix(gctx.encrypt_str(s1, seed=80))
+    h2 = gctx.upload_radix(gctx.encrypt_str(s2, seed=81))
+    outs = []
+    for _ in range(3):
+        o1, _ = gctx.has_match(h1, "/abc/")
+        o2, _ = gctx.has_match(h2, "/abc/")
+        n1 = gctx.not_(o1)
+        orr = gctx.or_(o1, o2)
+        outs.append([gctx.download_radix(x) for x in (o1, o2, n1, orr)])
+        for x in (o1, o2, n1, orr):
+            gctx.release(x)
+    dec = [[gctx.decrypt_radix(w) for w in ws] for ws in outs]
+    assert dec == [[1, 0, 0, 1]] * 3
+    assert all(np.array_equal(outs[0][i], outs[r][i]) for r in (1, 2) for i in range(2))
+    gctx.set_async(False)
+    try:
+        ob, _ = gctx.has_match(h1, "/abc/")
+        assert np.array_equal(gctx.download_radix(ob), outs[0][0])
+    finally:
+        gctx.set_async(True)
+    for h in h1 + h2 + [ob]:
+        gctx.release(h)
+
+
 def test_profiling_timers(gctx):
     """Profiling mode (bench.py's timed region): per-level KS / BR event timers
     accumulate one launch per level and the match result is unchanged."""
