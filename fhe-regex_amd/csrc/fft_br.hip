@@ -346,7 +346,9 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl)
     if constexpr (fperm_ok<M, E, PF, PT>()) {
         // a pre-barrier would also order the next exchange's writes: keep the plan's barriers
         static_assert(!PRE, "register exchanges replace only exchanges without a pre-barrier");
+#ifndef FR_FFT_NOPERMX  // timing experiment only (wrong results): register exchanges skipped
         fperm_exchange<M, E, PF, PT>(x);
+#endif
     } else {
 #ifdef FR_FFT_NOXCHG  // timing experiment only (wrong results): LDS exchanges skipped
         return;
@@ -794,7 +796,11 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
             for (int h = 1; h < 3; ++h)  // uniform quarter turn
                 fft::psi_quadrant(bre[h - 1][m >> 2], bim[h - 1][m >> 2], ((h == 1 ? ei : ej) * sm) & 3u, cr[h], ci[h]);
+#ifdef FR_FFT_NOC0  // timing experiment only (wrong results): no pair-monomial product
+            cr[0] = cr[1] + cr[2], ci[0] = ci[1];
+#else
             fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
+#endif
             // per row r: K_r = sum_g B_g[r][P] (c_g - 1), g ascending; then
             // z = D_P K_P + sum_(r != P, ascending) D_r K_r  (own row first).
             // 16 (K + 1) VALU per slot (k = 1: 32, against 36 for sum_g (c_g - 1) y_g)
