@@ -166,7 +166,11 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 //  * the MAC's key products computed in the shadow of the forward cross-wave exchange,
 //    the next step's key loaded right after them: 1.38 ms (ab_kearly.log);
 //  * k = 1 throughput shapes with E = 8 / 16 (two waves / one wave per polynomial): 12.0 /
-//    13.4 against 10.8 ms per 2048 bootstraps (ab_lane_elems_k1.log).
+//    13.4 against 10.8 ms per 2048 bootstraps (ab_lane_elems_k1.log);
+//  * a 16-wave latency shape (E = 2, build with -DFR_LAT_E2): 2.03 ms with the twiddles
+//    from LDS, 2.27 with them in registers (spilled at the 128-VGPR cap of 4 waves per
+//    SIMD), against 1.34: nine exchanges per transform, three of them cross-wave
+//    (ab_lat_e2_16wave.log).
 
 template <int M, int E>
 constexpr int ftw_index(int s, int m) {
@@ -486,7 +490,7 @@ constexpr int fbr_tp_groups() {
 // waves per SIMD the register allocation must allow
 template <int N, int K, int E, bool LAT>
 constexpr int fbr_min_waves() {
-    if (LAT) return 2;
+    if (LAT) return E == 2 ? 4 : 2;  // E = 2 (FR_LAT_E2 experiment): 16 waves, 4 per SIMD
     if (K == 1) return E == 4 ? 4 : 2;
     return E == 4 ? 3 : 2;  // k = 2: 2 x 6 waves (E = 4); E = 8: the one-slot-ahead loads need > 168 VGPRs
 }
@@ -560,7 +564,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     constexpr int M = N / 2;
     using G = FGeo<M, E>;
     static_assert(fexchanges_conflict_free<M, E>(), "LDS maps must make every exchange conflict-free");
-    static_assert(!LAT || E == 4, "the latency shape holds a step's GGSW values in registers: E = 4");
+    static_assert(!LAT || E == 4 || E == 2, "the latency shape holds a step's GGSW values in registers: E = 4 (2: experiment)");
+    constexpr int NB = E >= 4 ? E / 4 : 1;  // psi bases per lane (slots m >> 2 share one)
     constexpr int T = M / E, NT = (K + 1) * T, LAST = G::NPH - 1, XL = G::XL;
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
     constexpr bool TWR = fbr_twr<K, LAT>();  // twiddles in registers
@@ -599,9 +604,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     const uint32_t bbar = mod_switch(in[n], LOG2N2);
     // leaf exponents mod M of this lane's slot bases (slots 4b): L(j) = 1 + 4 brv(j)
     // (fft::Tables::leaf, checked against the table in tests/test_fft.py)
-    uint32_t Lb[E / 4];
+    uint32_t Lb[NB];
 #pragma unroll
-    for (int bb = 0; bb < E / 4; ++bb)
+    for (int bb = 0; bb < NB; ++bb)
         Lb[bb] = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 4 * bb)) >> (32 - G::LOG))) & (uint32_t)(M - 1);
     __syncthreads();
 
@@ -702,7 +707,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         }
         const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
         const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
-        constexpr int NB = E / 4;
         double bre[2][NB], bim[2][NB];
         auto psi_factors = [&]() {
 #pragma unroll
@@ -913,6 +917,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 // k = 1: E = 4 only (its transforms are radix-4 in the inverse, fradix4)
 template <int N, int K, int E>
 constexpr bool fft_shape_ok() {
+#ifdef FR_LAT_E2  // experiment: a 16-wave latency shape (E = 2) for k = 1; host keygen only
+    if (K == 1 && N == 2048 && E == 2) return true;
+#endif
     return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
 }
 static bool fft_supported(int K, int N, int E) {
@@ -945,6 +952,9 @@ void Device::init_fft() {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
         fft_attr<N, K, 4, true>();
         fft_attr<N, K, 4, false>();
+#ifdef FR_LAT_E2
+        if constexpr (fft_shape_ok<N, K, 2>()) fft_attr<N, K, 2, true>();
+#endif
         if constexpr (fft_shape_ok<N, K, 8>()) fft_attr<N, K, 8, false>();
     });
 
@@ -968,11 +978,17 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
     // slot order -> per-lane order [poly][m][lane] (one copy per lane geometry E):
     // lane tl's element m is slot idx<LAST>(tl, m), so each load of a wave is 1 KB contiguous
     std::vector<fft::c64> lanes(four.size());
-    for (int E : {16, 8, 4}) {
+    for (int E : {16, 8, 4, 2}) {
+#ifdef FR_LAT_E2
+        const bool e2 = E == 2 && p_.k == 1;  // the experiment's latency layout, in the E = 16 slot
+#else
+        const bool e2 = false;
+#endif
+        if (E == 2 && !e2) continue;
         double*& dst = d_fbsk_[fbsk_index(E)];
         (void)hipFree(dst);
         dst = nullptr;
-        if (!fft_supported(p_.k, N, E) || !fbsk_needed(E)) continue;
+        if (!e2 && (!fft_supported(p_.k, N, E) || !fbsk_needed(E))) continue;
         const int T = M / E;
         int e = 0;
         while ((1 << e) < E) ++e;
@@ -1003,6 +1019,12 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
         using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
         // small launches (at most one bootstrap per CU): the latency shape
+#ifdef FR_LAT_E2
+        if (n <= fft_small_ && K == 1) {
+            go(std::integral_constant<int, 2>{}, std::true_type{});
+            return;
+        }
+#endif
         if (n <= fft_small_) go(I4{}, std::true_type{});
         else if (fft_e_ == 4) go(I4{}, std::false_type{});
         else go(I8{}, std::false_type{});

@@ -229,7 +229,7 @@ constexpr LdsMap make_b128_map(int LOG, int e, int H, int x, int nph, int V = 0)
     return m;
 }
 struct LdsMaps {
-    LdsMap m[8];
+    LdsMap m[12];
     int ch;
 };
 constexpr LdsMaps make_lds_maps(int LOG, int e, int H, int nph, int GB, int V = 0) {

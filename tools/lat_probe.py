@@ -16,6 +16,8 @@ with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
 k, N = (2, 1024) if os.environ.get("FR_PARAMS") == "k2n1024" else (1, 2048)
 ctx = F.Context(0, params=F.default_params(k=k, N=N))
 ctx.load_client_key(blob)
+if os.environ.get("FR_LAT_PROBE_HOSTKEY"):  # keys through the host upload path (experiment layouts)
+    ctx.set_keygen(F.KEYGEN_HOST)
 ctx.gen_server_key(42)
 hs = ctx.upload_bool(ctx.encrypt_blocks([i % 16 for i in range(64)], seed=3))
 out = {}
