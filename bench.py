@@ -538,15 +538,17 @@ def main():
     br_ms = t_after["br_ms"] - t_before["br_ms"]
     br_launches = t_after["br_launches"] - t_before["br_launches"]
     br_gates = t_after["br_gates"] - t_before["br_gates"]
-    lat = {kk: t_after[kk] - t_before[kk] for kk in ("lat_br_ms", "lat_launches", "lat_gates")}
+    lat = {kk: t_after[kk] - t_before[kk] for kk in ("lat_br_ms", "lat_launches", "lat_gates",
+                                                     "pair_br_ms", "pair_launches", "pair_gates")}
     cus = 256
 
-    def shape_line(ms, launches, gates):
-        """one launch shape: algorithmic TFLOP/s, also per active CU (min(bootstraps, 256) CUs)"""
+    def shape_line(ms, launches, gates, per_wg=1):
+        """one launch shape: algorithmic TFLOP/s, also per active CU (min(workgroups, 256) CUs; per_wg
+        bootstraps per workgroup)"""
         if ms <= 0 or launches == 0:
             return None
         tf = gates * fpp / (ms / 1e3) / 1e12
-        active = min(gates / launches, cus)
+        active = min(gates / launches / per_wg, cus)
         return {"launches": int(launches), "bootstraps_per_launch": gates / launches, "avg_ms": ms / launches,
                 "achieved_tflops": tf, "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
                 "frac_of_active_cus": tf / (FP64_VECTOR_PEAK_TFLOPS * active / cus)}
@@ -626,8 +628,10 @@ def main():
             "br_gates_per_launch": br_gates / max(br_launches, 1),
             "per_shape": {
                 "latency": shape_line(lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
-                "throughput": shape_line(br_ms - lat["lat_br_ms"], br_launches - lat["lat_launches"],
-                                         br_gates - lat["lat_gates"]),
+                "pair": shape_line(lat["pair_br_ms"], lat["pair_launches"], lat["pair_gates"], 2),
+                "throughput": shape_line(br_ms - lat["lat_br_ms"] - lat["pair_br_ms"],
+                                         br_launches - lat["lat_launches"] - lat["pair_launches"],
+                                         br_gates - lat["lat_gates"] - lat["pair_gates"]),
             },
             "valu_issue": None if not pmc or pmc.get("valu_per_cu_clk") is None else {
                 "achieved": pmc["valu_per_cu_clk"],

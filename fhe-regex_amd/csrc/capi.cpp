@@ -1667,6 +1667,17 @@ int fr_device_timers_latency(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, 
         if (br_gates) *br_gates = t.lat_gates;
     })
 }
+int fr_device_timers_pair(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, uint64_t* br_gates) {
+    FR_TRY({
+        NEED(ctx);
+        Device& dev = ctx->device();
+        dev.sync();
+        const DeviceTimers& t = dev.timers();
+        if (br_ms) *br_ms = t.pair_br_ms;
+        if (br_launches) *br_launches = t.pair_launches;
+        if (br_gates) *br_gates = t.pair_gates;
+    })
+}
 int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates) {
     FR_TRY({
         NEED(ctx);

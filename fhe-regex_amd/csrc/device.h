@@ -37,6 +37,9 @@ struct DeviceTimers {
     // the part of the above in latency-shape launches (at most one bootstrap per CU)
     double lat_br_ms = 0;
     uint64_t lat_launches = 0, lat_gates = 0;
+    // the part in pair-shape launches (k = 1, two bootstraps per workgroup)
+    double pair_br_ms = 0;
+    uint64_t pair_launches = 0, pair_gates = 0;
 };
 
 struct ClientKey;
@@ -161,6 +164,9 @@ class Device {
     // psi quadrant table, leaf exponents (fft.h)
     int fft_e_ = 4;           // complex points per lane in the throughput shape (4, 8 or 16)
     size_t fft_small_ = 256;  // launches of at most this many bootstraps use the latency shape
+    // k = 1: larger launches up to this many use the pair shape (2 per workgroup; every size
+    // by default: profiles/r03/ab_pair_shape.log)
+    size_t fft_pair_ = SIZE_MAX;
     // Fourier BSK, one copy per lane geometry in use: [0] E = 4 (latency shape, always),
     // [1] E = 8, [2] E = 16 (the throughput shape's when fft_e_ is that)
     double* d_fbsk_[3] = {nullptr, nullptr, nullptr};
@@ -180,9 +186,10 @@ class Device {
     struct PendingTimer {
         void* ev[3];
         size_t gates, outs;
-        bool lat;
+        bool lat, pair;
     };
     bool latency_shape(size_t n) const;  // launch_br's shape choice for n bootstraps
+    bool pair_shape(size_t n) const;     // (FFT ring, k = 1: the pair shape)
     std::vector<PendingTimer> pending_;
     std::vector<void*> event_pool_;
     uint64_t* d_ks_ = nullptr;

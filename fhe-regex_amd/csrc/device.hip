@@ -1276,6 +1276,7 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
 }
 
 bool Device::latency_shape(size_t n) const { return n <= (p_.ring == FR_RING_FFT ? fft_small_ : small_batch_); }
+bool Device::pair_shape(size_t n) const { return p_.ring == FR_RING_FFT && !latency_shape(n) && n <= fft_pair_; }
 
 void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
     if (p_.ring == FR_RING_FFT) {
@@ -1384,6 +1385,7 @@ void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n)
         HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[2], STREAM));
         t.gates = n;
         t.lat = latency_shape(n);
+        t.pair = pair_shape(n);
         t.outs = 0;
         for (size_t i = 0; i < n; ++i) t.outs += host[i].n_out;
         pending_.push_back(t);
@@ -1432,6 +1434,11 @@ void Device::resolve_timers() {
             timers_.lat_br_ms += br;
             timers_.lat_launches += 1;
             timers_.lat_gates += t.gates;
+        }
+        if (t.pair) {
+            timers_.pair_br_ms += br;
+            timers_.pair_launches += 1;
+            timers_.pair_gates += t.gates;
         }
         for (auto* e : t.ev) event_pool_.push_back(e);
     }

@@ -154,6 +154,10 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_LAT_PF2
 #define FR_LAT_PF2 2
 #endif
+// pair shape: the forward phase after which a step's third GGSW group loads
+#ifndef FR_PAIR_LOAD
+#define FR_PAIR_LOAD 2
+#endif
 // latency shape, k = 1: the lane's twiddles in registers (1) or read from LDS (0)
 #ifndef FR_LAT_TWR
 #define FR_LAT_TWR 1
@@ -344,14 +348,17 @@ constexpr bool fxkeep_ok() {
     }
     return true;
 }
-template <int M, int E, int PF, int PT, bool PRE, bool XK = false>
-__device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl) {
+// B bootstraps per workgroup (pair shape: B = 2), bootstrap b's rows at row + b BS: one
+// barrier serves the exchanges of all B
+template <int M, int E, int PF, int PT, bool PRE, bool XK, int B, int BS>
+__device__ __forceinline__ void fexchange(double2 (&x)[B][E], double2* row, int tl) {
     using G = FGeo<M, E>;
     if constexpr (fperm_ok<M, E, PF, PT>()) {
         // a pre-barrier would also order the next exchange's writes: keep the plan's barriers
         static_assert(!PRE, "register exchanges replace only exchanges without a pre-barrier");
 #ifndef FR_FFT_NOPERMX  // timing experiment only (wrong results): register exchanges skipped
-        fperm_exchange<M, E, PF, PT>(x);
+#pragma unroll
+        for (int b = 0; b < B; ++b) fperm_exchange<M, E, PF, PT>(x[b]);
 #endif
     } else {
 #ifdef FR_FFT_NOXCHG  // timing experiment only (wrong results): LDS exchanges skipped
@@ -370,20 +377,28 @@ __device__ __forceinline__ void fexchange(double2 (&x)[E], double2* row, int tl)
         if constexpr (XK && fxkeep_ok<M, E, PF, PT>()) {  // the kept element: wave-uniform branches around its store and load
             const int q = __builtin_amdgcn_readfirstlane((tl >> 6) & (E - 1));
 #pragma unroll
-            for (int m = 0; m < E; ++m)
-                if (m != q) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+            for (int b = 0; b < B; ++b)
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    if (m != q) rf[b * BS + G::template at<X>(G::template moff<PF>(m))] = x[b][m];
             __syncthreads();
 #pragma unroll
-            for (int m = 0; m < E; ++m)
-                if (m != q) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
+            for (int b = 0; b < B; ++b)
+#pragma unroll
+                for (int m = 0; m < E; ++m)
+                    if (m != q) x[b][m] = rt[b * BS + G::template at<X>(G::template moff<PT>(m))];
             return;
         }
 #pragma unroll
-        for (int m = 0; m < E; ++m) rf[G::template at<X>(G::template moff<PF>(m))] = x[m];
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int m = 0; m < E; ++m) rf[b * BS + G::template at<X>(G::template moff<PF>(m))] = x[b][m];
         if constexpr (fwave_local<M, E, PF, PT>() && G::wave_top(PF)) fwave_sync();
         else __syncthreads();
 #pragma unroll
-        for (int m = 0; m < E; ++m) x[m] = rt[G::template at<X>(G::template moff<PT>(m))];
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int m = 0; m < E; ++m) x[b][m] = rt[b * BS + G::template at<X>(G::template moff<PT>(m))];
     }
 }
 // barrier plan as in device.hip: only the first exchange of a transform and
@@ -416,27 +431,44 @@ constexpr bool fexchanges_conflict_free() {
 // hook(integral_constant<p>) runs after phase p's butterflies (before its exchange).
 // CARRY: a pre-barrier owed by a register exchange (which writes no LDS) moves to the
 // next LDS exchange's write.
-template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false, class Hook>
-__device__ __forceinline__ void fforward_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
+// B, BS: B transforms side by side (rows b BS apart), their exchanges sharing barriers.
+template <int M, int E, int p, bool NOPRE, bool TWR, int B, int BS, bool CARRY = false, class Hook>
+__device__ __forceinline__ void fforward_from(double2 (&x)[B][E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, int tl, Hook&& hook) {
-    if constexpr (TWR) ffwd_phase_r<M, E, p>(x, twr);
-    else ffwd_phase<M, E, p>(x, tw, tl);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        if constexpr (TWR) ffwd_phase_r<M, E, p>(x[b], twr);
+        else ffwd_phase<M, E, p>(x[b], tw, tl);
+    }
     hook(std::integral_constant<int, p>{});
     if constexpr (p + 1 < FGeo<M, E>::NPH) {
         constexpr bool pre = !NOPRE && (ffwd_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p + 1>();
-        fexchange<M, E, p, p + 1, reg ? false : pre, !NOPRE>(x, row, tl);
-        fforward_from<M, E, p + 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, tl, hook);
+        fexchange<M, E, p, p + 1, reg ? false : pre, !NOPRE, B, BS>(x, row, tl);
+        fforward_from<M, E, p + 1, NOPRE, TWR, B, BS, reg && pre>(x, row, twr, tw, tl, hook);
     }
 }
-template <int M, int E, int p, bool NOPRE, bool TWR, bool CARRY = false>
-__device__ __forceinline__ void finverse_from(double2 (&x)[E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
+template <int M, int E, int p, bool NOPRE, bool TWR, int B, int BS, bool CARRY = false>
+__device__ __forceinline__ void finverse_from(double2 (&x)[B][E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, const double2* twc, int tl) {
-    if constexpr (TWR) finv_phase_r<M, E, p>(x, twr);
-    else finv_phase_lds<M, E, p>(x, tw, twc, tl);
+    if constexpr (TWR && B > 1 && fradix4<M, E>()) {
+        // pair shape: cc = c ca recomputed per phase (20 fewer live VGPRs; the same
+        // fft::cmul as ftw_load_phase, so the same bits), shared by the B transforms
+        const double2 c = twr.v[3 * p], ca = twr.v[3 * p + 1];
+        double2 cc;
+        fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+#pragma unroll
+        for (int b = 0; b < B; ++b) cinv_r4(x[b], c, ca, cc);
+    } else {
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            if constexpr (TWR) finv_phase_r<M, E, p>(x[b], twr);
+            else finv_phase_lds<M, E, p>(x[b], tw, twc, tl);
+        }
+    }
     if constexpr (p > 0) {
         constexpr bool pre = !NOPRE && (finv_pre<M, E, p>() || CARRY), reg = fperm_ok<M, E, p, p - 1>();
-        fexchange<M, E, p, p - 1, reg ? false : pre, !NOPRE>(x, row, tl);
-        finverse_from<M, E, p - 1, NOPRE, TWR, reg && pre>(x, row, twr, tw, twc, tl);
+        fexchange<M, E, p, p - 1, reg ? false : pre, !NOPRE, B, BS>(x, row, tl);
+        finverse_from<M, E, p - 1, NOPRE, TWR, B, BS, reg && pre>(x, row, twr, tw, twc, tl);
     }
 }
 
@@ -454,6 +486,12 @@ constexpr int fbr_threads() {
 //    inverse: 3 barriers per step instead of 5) in LDS.  k = 1 keeps the lane's
 //    twiddles in registers (TWR); k = 2 reads them from LDS (the 36 GGSW values
 //    take the registers).
+//  * pair (k = 1, B = 2; launches between the latency shape's limit and fft_pair_): the
+//    latency geometry with two bootstraps per workgroup.  One set of key loads, twiddle
+//    registers and barriers serves both (the two workgroups a CU would run side by side
+//    in the throughput shape each load the whole key and wait at their own barriers), and
+//    the two transforms give each other's exchanges independent work.  LDS: both row
+//    sets per bootstrap (139 KB) + the quadrant psi table; twiddles load from global once.
 //  * throughput (k = 1, E = 4: 8 waves, 128 VGPRs; E = 8: 4 waves): two workgroups per
 //    CU (<= 80 KB of LDS each) hide each other's barriers and loads; a slot's
 //    GGSW values are loaded one slot ahead in the MAC; psi^k from the quadrant
@@ -476,11 +514,15 @@ template <int N, int K, int E, bool LAT>
 constexpr int fbr_twc_entries() {
     return fradix4<N / 2, E>() && !fbr_twr<K, LAT>() ? N / 4 : 0;
 }
-template <int N, int K, int E, bool LAT>
+// LDS of a shape with B bootstraps per workgroup.  The pair shape (B = 2) keeps the
+// latency shape's two row sets per bootstrap (139 KB at k = 1) by dropping the forward
+// twiddle table (its registers load from global memory once) and using the quadrant
+// psi table; its multi-value terms live in the inverse rows after the loop.
+template <int N, int K, int E, bool LAT, int B = 1>
 constexpr size_t fbr_smem_bytes() {
-    return 16 * ((LAT ? 2 : 1) * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (size_t)N / 2 +
-                 (LAT ? (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
-           16 * MAX_OUT + 2 * 1026 + 4 * 17 * MAX_OUT + 2 * 514;
+    return 16 * ((LAT ? 2 : 1) * B * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (B == 1 ? (size_t)N / 2 : 0) +
+                 (LAT && B == 1 ? (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
+           B * (16 * MAX_OUT + 2 * 1026) + (B == 1 ? 4 * 17 * MAX_OUT : 0) + 2 * 514;
 }
 // workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
 template <int K, int E>
@@ -556,40 +598,56 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
     return acc;
 }
 
-template <int N, int K, int E, bool LAT>
+template <int N, int K, int E, bool LAT, int B = 1>
 __global__ void __launch_bounds__((fbr_threads<N, K, E>()), (fbr_min_waves<N, K, E, LAT>()))
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
-                   const double2* __restrict__ bsk, const double2* __restrict__ tw_g, const double2* __restrict__ psi_g,
-                   const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena, int slot_stride) {
+                   int n_gates, const double2* __restrict__ bsk, const double2* __restrict__ tw_g,
+                   const double2* __restrict__ psi_g, const uint16_t* __restrict__ leaf_g, uint64_t* __restrict__ arena,
+                   int slot_stride) {
     constexpr int M = N / 2;
     using G = FGeo<M, E>;
     static_assert(fexchanges_conflict_free<M, E>(), "LDS maps must make every exchange conflict-free");
     static_assert(!LAT || E == 4 || E == 2, "the latency shape holds a step's GGSW values in registers: E = 4 (2: experiment)");
+    static_assert(B == 1 || (B == 2 && LAT && K == 1 && E == 4), "pair shape: the k = 1 latency geometry");
     constexpr int NB = E >= 4 ? E / 4 : 1;  // psi bases per lane (slots m >> 2 share one)
     constexpr int T = M / E, NT = (K + 1) * T, LAST = G::NPH - 1, XL = G::XL;
     constexpr int LOG2N2 = G::LOG + 2;  // log2(2N)
     constexpr bool TWR = fbr_twr<K, LAT>();  // twiddles in registers
+    constexpr int BS = (K + 1) * G::NP;      // one bootstrap's exchange rows
+    constexpr bool PSIQ = !LAT || B > 1;     // psi^k from the quadrant table (k < N/2) + quarter turns
     extern __shared__ __attribute__((aligned(16))) double2 fsm[];
-    double2* xbuf = fsm;                  // K+1 rows of NP complex: row P at P * NP
-    double2* ibuf = LAT ? xbuf + (K + 1) * G::NP : xbuf;  // inverse-transform rows (latency shape: separate)
-    double2* tw = xbuf + (LAT ? 2 : 1) * (K + 1) * G::NP;  // M forward twiddles
-    constexpr int NPSI = LAT ? N : N / 2;
-    double2* psi = tw + M;                // psi^k, k < NPSI
+    double2* xbuf = fsm;                  // B x (K+1) rows of NP complex: bootstrap b, row P at b BS + P NP
+    double2* ibuf = LAT ? xbuf + B * BS : xbuf;  // inverse-transform rows (latency shapes: separate)
+    double2* tw = xbuf + (LAT ? 2 : 1) * B * BS;  // M forward twiddles (B = 1)
+    constexpr int NPSI = PSIQ ? N / 2 : N;
+    double2* psi = tw + (B == 1 ? M : 0);  // psi^k, k < NPSI
     double2* twc = psi + NPSI;            // radix-4 products c ca (fbr_twc_entries)
     constexpr int NTWC = fbr_twc_entries<N, K, E, LAT>();
-    uint8_t* lut = (uint8_t*)(twc + NTWC);             // 16 * n_out
-    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);  // n (<= 1024), zero-padded to even
-    uint32_t* wterms = (uint32_t*)(abar + 1026);       // multi-value terms, 16 per output
-    int* wcnt = (int*)(wterms + 16 * MAX_OUT);
-    uint16_t* nxt = (uint16_t*)(wcnt + MAX_OUT);  // (latency shape) next unskipped step >= t, t <= steps
+    uint8_t* lut = (uint8_t*)(twc + NTWC);                 // [B][16 * MAX_OUT]
+    uint16_t* abar = (uint16_t*)(lut + B * 16 * MAX_OUT);  // [B][1026]: n (<= 1024), zero-padded to even
+    uint32_t* wterms = B == 1 ? (uint32_t*)(abar + 1026) : (uint32_t*)ibuf;  // multi-value terms, [B][16 MAX_OUT]
+    int* wcnt = (int*)(wterms + B * 16 * MAX_OUT);                           // [B][MAX_OUT]
+    uint16_t* nxt = B == 1 ? (uint16_t*)(wcnt + MAX_OUT) : abar + B * 1026;  // (latency shapes) next unskipped step
 
     const int tid = threadIdx.x;
     const int P = __builtin_amdgcn_readfirstlane(tid / T), tl = tid % T;  // wave-uniform polynomial
-    const int g = blockIdx.x;
-    const uint64_t* in = ks + (size_t)g * ks_stride;
-    const int n_out = gates[g].n_out;
-    const int kind = gates[g].direct;
-    for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
+    // bootstrap b of this workgroup: gate B blockIdx + b (an odd count's last pair repeats its
+    // gate and writes it once)
+    int gb[B];
+    bool has[B];
+    const uint64_t* in[B];
+    int n_out[B], kind[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const int gi = B * (int)blockIdx.x + b;
+        has[b] = gi < n_gates;
+        gb[b] = has[b] ? gi : B * (int)blockIdx.x;
+        in[b] = ks + (size_t)gb[b] * ks_stride;
+        n_out[b] = gates[gb[b]].n_out;
+        kind[b] = gates[gb[b]].direct;
+    }
+    if constexpr (B == 1)
+        for (int i = tid; i < M; i += NT) tw[i] = tw_g[i];
     for (int i = tid; i < NPSI; i += NT) psi[psi_slot(i)] = psi_g[i];
     // twc[2^s0 + b] = tw[2^s0 + b] * tw[2^(s0+1) + 2b] for even s0 (fft::cmul, as the oracle)
     for (int i = 1 + tid; i < NTWC; i += NT) {
@@ -598,10 +656,16 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         const double2 c = tw_g[i], ca = tw_g[(2 << s0) + 2 * b];
         fft::cmul(c.x, c.y, ca.x, ca.y, twc[i].x, twc[i].y);
     }
-    for (int i = tid; i < 16 * n_out; i += NT) lut[i] = gates[g].lut[i / 16][i % 16];
-    for (int i = tid; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
-    if (tid == 0) abar[n] = 0;  // pad an odd n
-    const uint32_t bbar = mod_switch(in[n], LOG2N2);
+    uint32_t bbar[B];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        uint8_t* lb = lut + b * 16 * MAX_OUT;
+        uint16_t* ab = abar + b * 1026;
+        for (int i = tid; i < 16 * n_out[b]; i += NT) lb[i] = gates[gb[b]].lut[i / 16][i % 16];
+        for (int i = tid; i < n; i += NT) ab[i] = (uint16_t)mod_switch(in[b][i], LOG2N2);
+        if (tid == 0) ab[n] = 0;  // pad an odd n
+        bbar[b] = mod_switch(in[b][n], LOG2N2);
+    }
     // leaf exponents mod M of this lane's slot bases (slots 4b): L(j) = 1 + 4 brv(j)
     // (fft::Tables::leaf, checked against the table in tests/test_fft.py)
     uint32_t Lb[NB];
@@ -612,21 +676,22 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 
     // accumulator (f64 torus, fft.h), natural order: lane holds coefficients j and
     // j + M for j = idx<0>(tl, m); mask polynomials 0, body (polynomial K) X^-bbar * V
-    double alo[E], ahi[E];
-    {
-        const bool direct = kind == JOB_DIRECT;
+    double alo[B][E], ahi[B][E];
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        const bool direct = kind[b] == JOB_DIRECT;
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int j = G::template idx<0>(tl, m);
             uint64_t v[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int s = (j + h * M + (int)bbar) & (2 * N - 1);
-                const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut);
+                const int s = (j + h * M + (int)bbar[b]) & (2 * N - 1);
+                const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut + b * 16 * MAX_OUT);
                 v[h] = s < N ? tv : (uint64_t)0 - tv;
             }
-            alo[m] = P == K ? fft::acc_of_torus(v[0]) : 0.0;
-            ahi[m] = P == K ? fft::acc_of_torus(v[1]) : 0.0;
+            alo[b][m] = P == K ? fft::acc_of_torus(v[0]) : 0.0;
+            ahi[b][m] = P == K ? fft::acc_of_torus(v[1]) : 0.0;
         }
     }
 
@@ -645,7 +710,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // and (k = 1) the lane's twiddles
     double2 gv[3][K + 1][LAT ? E : 1];
     FTwr<M, TWR ? E : 2> twr;
-    if constexpr (TWR) ftw_load_phase<M, E, 0>(twr, tw, tl);
+    if constexpr (TWR) ftw_load_phase<M, E, 0>(twr, B == 1 ? tw : tw_g, tl);
 #ifdef FR_BR_TIMING
     uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
@@ -678,10 +743,20 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // control flow around the prefetch, which keeps it after the MAC's last use).
     constexpr int NPF = LAT ? (K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;
     constexpr bool LATPF = NPF > 0;
+    static_assert(B == 1 || NPF == 2, "pair shape: two groups a step ahead, the third in the forward FFT");
+    // step t is skipped when every bootstrap's pair is (0, 0): X^0 acc - acc = 0.  The pair
+    // shape runs a step that is zero for one bootstrap only: its factors c - 1 are exact
+    // zeros, so its MAC output is 0 and the accumulate adds +-0.
+    auto idle = [&](int t) {
+        uint32_t z = 0;
+#pragma unroll
+        for (int b = 0; b < B; ++b) z |= abar[b * 1026 + 2 * t] | abar[b * 1026 + 2 * t + 1];
+        return z == 0;
+    };
     if constexpr (LATPF) {
         for (int t = tid; t <= steps; t += NT) {
             int tt = t;
-            while (tt < steps && (abar[2 * tt] | abar[2 * tt + 1]) == 0) ++tt;
+            while (tt < steps && idle(tt)) ++tt;
             nxt[t] = (uint16_t)tt;
         }
         __syncthreads();
@@ -689,7 +764,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, t0 < steps ? t0 : 0);
     }
     for (int t = 0; t < steps; ++t) {
-        if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // X^0 acc - acc = 0 (uniform branch)
+        if (idle(t)) continue;  // (uniform branch)
         FBR_STAMP(0);
         // the step's byte offset in the key (uniform: soffset of every load)
         const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
@@ -697,49 +772,61 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // phases FR_LAT_LOAD1 / FR_LAT_LOAD2 (3: none).  k = 1, NPF = 2: the third group at the
         // top (tools/ab_libs.sh: 1.34 ms; after forward phase 0 / 2 / 3: 1.33 / 1.38 / 1.38 ms;
         // after the previous inverse: 1.35 ms); k = 2 keeps it after phase 3 (1.67 vs 1.71 ms)
-        constexpr int G_TOP = !LAT ? 3 : (NPF < 2 || K == 1) ? NPF : 3;
-        constexpr int G_L1 = !LAT ? 3 : G_TOP + 1 < 3 ? G_TOP + 1 : 3;
-        constexpr int G_L2 = !LAT ? 3 : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
+        // The pair shape loads its third group after forward phase FR_PAIR_LOAD (the pair's
+        // 64 live transform values leave no room for it across the whole transform).
+        constexpr int G_TOP = !LAT || B > 1 ? 3 : (NPF < 2 || K == 1) ? NPF : 3;
+        constexpr int G_L1 = !LAT ? 3 : B > 1 ? NPF : G_TOP + 1 < 3 ? G_TOP + 1 : 3;
+        constexpr int G_L2 = !LAT || B > 1 ? 3 : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
+        constexpr int PH_L1 = B > 1 ? FR_PAIR_LOAD : FR_LAT_LOAD1;
         if constexpr (G_TOP < 3) {
             __builtin_amdgcn_sched_barrier(0);
             load_ggsw(G_TOP, t);
             __builtin_amdgcn_sched_barrier(0);
         }
-        const uint32_t ai = abar[2 * t], aj = abar[2 * t + 1];
-        const uint32_t ei = __builtin_amdgcn_readfirstlane(ai), ej = __builtin_amdgcn_readfirstlane(aj);
-        double bre[2][NB], bim[2][NB];
+        uint32_t ei[B], ej[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+            ei[b] = __builtin_amdgcn_readfirstlane((uint32_t)abar[b * 1026 + 2 * t]);
+            ej[b] = __builtin_amdgcn_readfirstlane((uint32_t)abar[b * 1026 + 2 * t + 1]);
+        }
+        double bre[B][2][NB], bim[B][2][NB];
         auto psi_factors = [&]() {
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int b = 0; b < B; ++b)
 #pragma unroll
-                for (int bb = 0; bb < NB; ++bb) {
-                    const uint32_t k = __umul24(h == 0 ? ei : ej, Lb[bb]) & (2 * N - 1);
-                    if constexpr (LAT) {  // psi^(k+N) = -psi^k: flip both signs
+                for (int h = 0; h < 2; ++h)
+#pragma unroll
+                    for (int bb = 0; bb < NB; ++bb) {
+                        const uint32_t k = __umul24(h == 0 ? ei[b] : ej[b], Lb[bb]) & (2 * N - 1);
+                        if constexpr (!PSIQ) {  // psi^(k+N) = -psi^k: flip both signs
 #ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
-                        const double2 c = make_double2((double)k, 0.5);
+                            const double2 c = make_double2((double)k, 0.5);
 #else
-                        const double2 c = psi[psi_slot((int)(k & (N - 1)))];
+                            const double2 c = psi[psi_slot((int)(k & (N - 1)))];
 #endif
-                        const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
-                        bre[h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
-                        bim[h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
-                    } else {
-                        const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
-                        fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h][bb], bim[h][bb]);
+                            const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
+                            bre[b][h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
+                            bim[b][h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
+                        } else {
+                            const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
+                            fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[b][h][bb], bim[b][h][bb]);
+                        }
                     }
-                }
         };
-        if constexpr (LAT) psi_factors();
+        if constexpr (LAT && B == 1) psi_factors();
         // 1. signed gadget digits, folded: x = d_j + i d_(j+M)
-        double2 x[E];
+        double2 x[B][E];
 #pragma unroll
-        for (int m = 0; m < E; ++m) x[m] = make_double2(fft::acc_digit<23>(alo[m]), fft::acc_digit<23>(ahi[m]));
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                x[b][m] = make_double2(fft::acc_digit<23>(alo[b][m]), fft::acc_digit<23>(ahi[b][m]));
         FBR_STAMP(1);
         // 2. forward FFT (latency shape: GGSW groups 1 and 2 issued at phase boundaries)
-        fforward_from<M, E, 0, LAT, TWR>(x, row, twr, tw, tl, [&](auto ph) {
+        fforward_from<M, E, 0, LAT, TWR, B, BS>(x, row, twr, tw, tl, [&](auto ph) {
             if constexpr (LAT) {
                 constexpr int p = decltype(ph)::value;
-                if constexpr (p == FR_LAT_LOAD1 && G_L1 < 3) {
+                if constexpr (p == PH_L1 && G_L1 < 3) {
                     __builtin_amdgcn_sched_barrier(0);
                     load_ggsw(G_L1, t);
                     __builtin_amdgcn_sched_barrier(0);
@@ -755,7 +842,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // 3. MAC with the three GGSWs of the pair and their monomial factors
 #ifndef FR_FFT_NOMACX  // timing experiment only (wrong results): no MAC exchange
 #pragma unroll
-        for (int m = 0; m < E; ++m) row_bl[G::template at<XL>(G::template moff<LAST>(m))] = x[m];
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int m = 0; m < E; ++m) row_bl[b * BS + G::template at<XL>(G::template moff<LAST>(m))] = x[b][m];
 #endif
         // throughput shapes: slot m's GGSW values, loaded one slot ahead (E = 8) or
         // at the top of the slot (E = 4, 128 VGPRs: the other workgroup hides the wait)
@@ -777,7 +866,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // itself is quadrant-reduced), so one lookup per (e, base) serves every slot.
         // latency shape: computed at the top of the step (the lookups' LDS latency hides
         // behind the digits and the forward FFT); throughput shapes: here (VGPR budget)
-        if constexpr (!LAT) psi_factors();
+        if constexpr (!LAT || B > 1) psi_factors();
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             double2 Bn[3][K + 1];
@@ -787,46 +876,50 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             } else if constexpr (!LAT) {
                 if (!PRE0 || m > 0) load_slot<M, T, K>(Bc, rs, sbase, P, m, lane_off);
             }
-            const double2 own = x[m];
-            double2 oth[K];
+#pragma unroll
+            for (int b = 0; b < B; ++b) {  // (the pair shape: both bootstraps on one set of key values)
+                const double2 own = x[b][m];
+                double2 oth[K];
 #pragma unroll
 #ifdef FR_FFT_NOMACX
-            for (int q = 0; q < K; ++q) oth[q] = make_double2(own.y, own.x);
+                for (int q = 0; q < K; ++q) oth[q] = make_double2(own.y, own.x);
 #else
-            for (int q = 0; q < K; ++q) oth[q] = orow_bl[q][G::template at<XL>(G::template moff<LAST>(m))];
+                for (int q = 0; q < K; ++q) oth[q] = orow_bl[q][b * BS + G::template at<XL>(G::template moff<LAST>(m))];
 #endif
-            const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
-            double cr[3], ci[3];
+                const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
+                double cr[3], ci[3];
 #pragma unroll
-            for (int h = 1; h < 3; ++h)  // uniform quarter turn
-                fft::psi_quadrant(bre[h - 1][m >> 2], bim[h - 1][m >> 2], ((h == 1 ? ei : ej) * sm) & 3u, cr[h], ci[h]);
+                for (int h = 1; h < 3; ++h)  // uniform quarter turn
+                    fft::psi_quadrant(bre[b][h - 1][m >> 2], bim[b][h - 1][m >> 2], ((h == 1 ? ei[b] : ej[b]) * sm) & 3u,
+                                      cr[h], ci[h]);
 #ifdef FR_FFT_NOC0  // timing experiment only (wrong results): no pair-monomial product
-            cr[0] = cr[1] + cr[2], ci[0] = ci[1];
+                cr[0] = cr[1] + cr[2], ci[0] = ci[1];
 #else
-            fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
+                fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
 #endif
-            // per row r: K_r = sum_g B_g[r][P] (c_g - 1), g ascending; then
-            // z = D_P K_P + sum_(r != P, ascending) D_r K_r  (own row first).
-            // 16 (K + 1) VALU per slot (k = 1: 32, against 36 for sum_g (c_g - 1) y_g)
-            double kor, koi, kxr[K], kxi[K];
+                // per row r: K_r = sum_g B_g[r][P] (c_g - 1), g ascending; then
+                // z = D_P K_P + sum_(r != P, ascending) D_r K_r  (own row first).
+                // 16 (K + 1) VALU per slot (k = 1: 32, against 36 for sum_g (c_g - 1) y_g)
+                double kor, koi, kxr[K], kxi[K];
 #pragma unroll
-            for (int gg = 0; gg < 3; ++gg) {
-                const double c1r = cr[gg] - 1.0, c1i = ci[gg];
-                const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
-                if (gg == 0) fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
-                else fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                for (int gg = 0; gg < 3; ++gg) {
+                    const double c1r = cr[gg] - 1.0, c1i = ci[gg];
+                    const double2 Bo = LAT ? gv[gg][0][LAT ? m : 0] : Bc[gg][0];
+                    if (gg == 0) fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                    else fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
 #pragma unroll
-                for (int q = 0; q < K; ++q) {
-                    const double2 Bx = LAT ? gv[gg][1 + q][LAT ? m : 0] : Bc[gg][1 + q];
-                    if (gg == 0) fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
-                    else fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
+                    for (int q = 0; q < K; ++q) {
+                        const double2 Bx = LAT ? gv[gg][1 + q][LAT ? m : 0] : Bc[gg][1 + q];
+                        if (gg == 0) fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
+                        else fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr[q], kxi[q]);
+                    }
                 }
-            }
-            double zr, zi;
-            fft::cmul(own.x, own.y, kor, koi, zr, zi);
+                double zr, zi;
+                fft::cmul(own.x, own.y, kor, koi, zr, zi);
 #pragma unroll
-            for (int q = 0; q < K; ++q) fft::cmac(oth[q].x, oth[q].y, kxr[q], kxi[q], zr, zi);
-            x[m] = make_double2(zr, zi);
+                for (int q = 0; q < K; ++q) fft::cmac(oth[q].x, oth[q].y, kxr[q], kxi[q], zr, zi);
+                x[b][m] = make_double2(zr, zi);
+            }
             if constexpr (!LAT) {
                 // keep the loads one slot ahead / in their slot, not all hoisted
                 __builtin_amdgcn_sched_barrier(0);
@@ -846,13 +939,15 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         }
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
-        finverse_from<M, E, LAST, LAT, TWR>(x, irow, twr, tw, twc, tl);
+        finverse_from<M, E, LAST, LAT, TWR, B, BS>(x, irow, twr, tw, twc, tl);
         FBR_STAMP(4);
 #pragma unroll
-        for (int m = 0; m < E; ++m) {
-            alo[m] = fft::acc_reduce(alo[m] + x[m].x);
-            ahi[m] = fft::acc_reduce(ahi[m] + x[m].y);
-        }
+        for (int b = 0; b < B; ++b)
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                alo[b][m] = fft::acc_reduce(alo[b][m] + x[b][m].x);
+                ahi[b][m] = fft::acc_reduce(ahi[b][m] + x[b][m].y);
+            }
         FBR_STAMP(5);
     }
 #ifdef FR_BR_TIMING
@@ -864,49 +959,60 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #endif
 
     // publish the accumulator as u64 [P][N] over the exchange rows
+    // (pair shape: bootstrap b's u64 rows at b (K+1) N, inside the forward rows; its terms in
+    // the inverse rows)
     __syncthreads();
     uint64_t* accs = (uint64_t*)xbuf;
 #pragma unroll
-    for (int m = 0; m < E; ++m) {
-        const int j = G::template idx<0>(tl, m);
-        accs[P * N + j] = fft::torus_of(alo[m]);
-        accs[P * N + j + M] = fft::torus_of(ahi[m]);
-    }
+    for (int b = 0; b < B; ++b)
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            accs[(b * (K + 1) + P) * N + j] = fft::torus_of(alo[b][m]);
+            accs[(b * (K + 1) + P) * N + j + M] = fft::torus_of(ahi[b][m]);
+        }
+    static_assert(B == 1 || 8 * B * (K + 1) * N <= 16 * B * BS, "pair shape: u64 rows inside the forward rows");
+#pragma unroll
+    for (int b = 0; b < B; ++b)
+        if (tid < n_out[b] && kind[b] == JOB_MULTI) {
+            // multi-value terms (device.hip lut_terms)
+            constexpr int box = N / 16, half = box / 2;
+            const uint8_t* lf = lut + b * 16 * MAX_OUT + 16 * tid;
+            uint32_t* terms = wterms + b * 16 * MAX_OUT + 16 * tid;
+            int nt = 0;
+            for (int tt = 1; tt <= 16; ++tt) {
+                const int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+                if (d != 0) terms[nt++] = (uint32_t)(tt < 16 ? tt * box - half : N - half) | ((uint32_t)(d + 128) << 16);
+            }
+            wcnt[b * MAX_OUT + tid] = nt;
+        }
     __syncthreads();
     constexpr int big = K * N;
-    if (kind != JOB_MULTI) {
-        uint64_t* out = arena + (size_t)gates[g].out_slot[0] * slot_stride;
-        const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
-        for (int c = tid; c <= big; c += NT) {
-            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
-            const int j = t == 0 ? 0 : N - t;
-            const uint64_t v = accs[pp * N + j];
-            out[c] = (t != 0 ? (uint64_t)0 - v : v) + (c == big ? post : 0);
+#pragma unroll
+    for (int b = 0; b < B; ++b) {
+        if (!has[b]) continue;
+        const uint64_t* ab = accs + b * (K + 1) * N;
+        if (kind[b] != JOB_MULTI) {
+            uint64_t* out = arena + (size_t)gates[gb[b]].out_slot[0] * slot_stride;
+            const uint64_t post = kind[b] == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
+            for (int c = tid; c <= big; c += NT) {
+                const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+                const int j = t == 0 ? 0 : N - t;
+                const uint64_t v = ab[pp * N + j];
+                out[c] = (t != 0 ? (uint64_t)0 - v : v) + (c == big ? post : 0);
+            }
+            continue;
         }
-        return;
-    }
-    if (tid < n_out) {
-        // multi-value terms (device.hip lut_terms)
-        constexpr int box = N / 16, half = box / 2;
-        const uint8_t* lf = lut + 16 * tid;
-        uint32_t* terms = wterms + 16 * tid;
-        int nt = 0;
-        for (int tt = 1; tt <= 16; ++tt) {
-            const int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
-            if (d != 0) terms[nt++] = (uint32_t)(tt < 16 ? tt * box - half : N - half) | ((uint32_t)(d + 128) << 16);
-        }
-        wcnt[tid] = nt;
-    }
-    __syncthreads();
-    for (int f = 0; f < n_out; ++f) {
-        const uint32_t* tf = wterms + 16 * f;
-        const int nt = wcnt[f];
-        uint64_t* out = arena + (size_t)gates[g].out_slot[f] * slot_stride;
-        for (int c = tid; c <= big; c += NT) {
-            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
-            const int j = t == 0 ? 0 : N - t;
-            const uint64_t v = w_step64<N>(accs + pp * N, tf, nt, j);
-            out[c] = t != 0 ? (uint64_t)0 - v : v;
+        for (int f = 0; f < n_out[b]; ++f) {
+            const uint32_t* tf = wterms + b * 16 * MAX_OUT + 16 * f;
+            const int nt = wcnt[b * MAX_OUT + f];
+            uint64_t* out = arena + (size_t)gates[gb[b]].out_slot[f] * slot_stride;
+            for (int c = tid; c <= big; c += NT) {
+                const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+                const int j = t == 0 ? 0 : N - t;
+                const uint64_t v = w_step64<N>(ab + pp * N, tf, nt, j);
+                out[c] = t != 0 ? (uint64_t)0 - v : v;
+            }
         }
     }
 }
@@ -926,12 +1032,12 @@ static bool fft_supported(int K, int N, int E) {
     return (K == 1 && N == 2048 && E == 4) || (K == 2 && N == 1024 && (E == 4 || E == 8));
 }
 
-template <int N, int K, int E, bool LAT>
+template <int N, int K, int E, bool LAT, int B = 1>
 static void fft_attr() {
-    static_assert(fbr_smem_bytes<N, K, E, LAT>() <= (LAT ? 160 * 1024 : 160 * 1024 / fbr_tp_groups<K, E>()),
+    static_assert(fbr_smem_bytes<N, K, E, LAT, B>() <= (LAT ? 160 * 1024 : 160 * 1024 / fbr_tp_groups<K, E>()),
                   "LDS per workgroup of the shape");
-    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, K, E, LAT>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbr_smem_bytes<N, K, E, LAT>()));
+    FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft<N, K, E, LAT, B>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbr_smem_bytes<N, K, E, LAT, B>()));
 }
 
 // run body(N, K) with the compile-time ring dimensions of the parameters
@@ -946,12 +1052,15 @@ void Device::init_fft() {
     if (p_.k == 2) fft_e_ = 8;  // one wave per polynomial: every transform exchange wave-local
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
+    if (const char* ev = std::getenv("FR_FFT_PAIR_BATCH")) fft_pair_ = (size_t)std::atol(ev);
+    if (p_.k != 1) fft_pair_ = 0;
     if (!fft_supported(p_.k, p_.N, fft_e_))
         throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N, E) in {(1, 2048, 4), (2, 1024, 4 or 8)}");
     fft_dispatch(p_, [&](auto nc, auto kc) {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
         fft_attr<N, K, 4, true>();
         fft_attr<N, K, 4, false>();
+        if constexpr (K == 1) fft_attr<N, K, 4, true, 2>();
 #ifdef FR_LAT_E2
         if constexpr (fft_shape_ok<N, K, 2>()) fft_attr<N, K, 2, true>();
 #endif
@@ -1008,26 +1117,30 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
     const hipStream_t s = (hipStream_t)stream;
     fft_dispatch(p_, [&](auto nc, auto kc) {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
-        auto go = [&](auto ec, auto lat) {
+        auto go = [&](auto ec, auto lat, auto bc) {
             constexpr int E = decltype(ec)::value;
             constexpr bool LAT = decltype(lat)::value;
-            if constexpr (fft_shape_ok<N, K, E>())
-            k_blind_rotate_fft<N, K, E, LAT><<<(unsigned)n, fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT>(), s>>>(
-                d_ks, p_.ks_stride(), p_.n, d_gates, (const double2*)d_fbsk_[fbsk_index(E)],
-                (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
+            constexpr int B = decltype(bc)::value;
+            if constexpr (fft_shape_ok<N, K, E>() && (B == 1 || K == 1))
+                k_blind_rotate_fft<N, K, E, LAT, B>
+                    <<<(unsigned)((n + B - 1) / B), fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT, B>(), s>>>(
+                        d_ks, p_.ks_stride(), p_.n, d_gates, (int)n, (const double2*)d_fbsk_[fbsk_index(E)],
+                        (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
         };
         using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
+        using B1 = std::integral_constant<int, 1>;
         // small launches (at most one bootstrap per CU): the latency shape
 #ifdef FR_LAT_E2
         if (n <= fft_small_ && K == 1) {
-            go(std::integral_constant<int, 2>{}, std::true_type{});
+            go(std::integral_constant<int, 2>{}, std::true_type{}, B1{});
             return;
         }
 #endif
-        if (n <= fft_small_) go(I4{}, std::true_type{});
-        else if (fft_e_ == 4) go(I4{}, std::false_type{});
-        else go(I8{}, std::false_type{});
+        if (n <= fft_small_) go(I4{}, std::true_type{}, B1{});
+        else if (n <= fft_pair_) go(I4{}, std::true_type{}, std::integral_constant<int, 2>{});  // (k = 1)
+        else if (fft_e_ == 4) go(I4{}, std::false_type{}, B1{});
+        else go(I8{}, std::false_type{}, B1{});
     });
     FFT_CHECK(hipGetLastError());
 }

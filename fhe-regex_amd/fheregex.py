@@ -171,6 +171,8 @@ _SIGS = {
                                    C.POINTER(C.c_uint64)]),
     "fr_device_timers_latency": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                            C.POINTER(C.c_uint64)]),
+    "fr_device_timers_pair": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                        C.POINTER(C.c_uint64)]),
     "fr_shard_plan": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t,
                                 C.POINTER(C.c_void_p), C.POINTER(MatchStats)]),
     "fr_shard_levels": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
@@ -492,8 +494,11 @@ class Context:
         _check(lib().fr_device_timers(self.h, C.byref(br), C.byref(ks), C.byref(nl), C.byref(ng)))
         lb, ll, lg = C.c_double(), C.c_uint64(), C.c_uint64()
         _check(lib().fr_device_timers_latency(self.h, C.byref(lb), C.byref(ll), C.byref(lg)))
+        pb, pl, pg = C.c_double(), C.c_uint64(), C.c_uint64()
+        _check(lib().fr_device_timers_pair(self.h, C.byref(pb), C.byref(pl), C.byref(pg)))
         return {"br_ms": br.value, "ks_ms": ks.value, "br_launches": nl.value, "br_gates": ng.value,
-                "lat_br_ms": lb.value, "lat_launches": ll.value, "lat_gates": lg.value}
+                "lat_br_ms": lb.value, "lat_launches": ll.value, "lat_gates": lg.value,
+                "pair_br_ms": pb.value, "pair_launches": pl.value, "pair_gates": pg.value}
 
     # single-stage device entry points
     def dev_keyswitch(self, lwes: np.ndarray) -> np.ndarray:

@@ -238,6 +238,9 @@ int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_lau
 /* The part of those blind-rotation timers spent in latency-shape launches (at
  * most one bootstrap per CU: one workgroup per CU). */
 int fr_device_timers_latency(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, uint64_t* br_gates);
+/* ... and in pair-shape launches (FFT ring, k = 1: two bootstraps per workgroup in the
+ * latency geometry, for batches above the latency shape's limit). */
+int fr_device_timers_pair(fr_ctx* ctx, double* br_ms, uint64_t* br_launches, uint64_t* br_gates);
 
 /* ----- one match split across ranks ----- */
 /* The reference folds ct_or over the branches of every start offset

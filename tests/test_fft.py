@@ -283,3 +283,39 @@ def test_fft_throughput_shape_bit_exact(key_blob, oracle_fft, point, keygen):
     got = ctx.dev_blind_rotate(ks, luts)
     for i in (0, 1, 150, 299):
         assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i
+
+
+def _shape_ctx(key_blob, point, monkeypatch, **env):
+    """A context whose launch-shape limits come from FR_FFT_* (read at creation)."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, str(v))
+    ctx = F.Context(device=0, params=F.default_params(k=point[0], N=point[1], ring=F.RING_FFT))
+    for k in env:
+        monkeypatch.delenv(k)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    return ctx
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("count", [301, 512])
+def test_fft_pair_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, count):
+    """The pair shape (k = 1: two bootstraps per workgroup sharing key loads, twiddles
+    and barriers; an odd count's last workgroup holds one) bit-exact against the oracle
+    on sampled rows and against the one-bootstrap throughput shape on every row, with
+    zero pairs in one bootstrap's coefficients but not its partner's (steps the pair
+    runs for one of them only)."""
+    if point[0] != 1:
+        pytest.skip("the pair shape is the k = 1 latency geometry")
+    pair = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_PAIR_BATCH=4096)
+    tp = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_PAIR_BATCH=0)
+    O = oracle_fft
+    rng = np.random.default_rng(count)
+    ks = rng.integers(0, 2**64 - 1, (count, O.n + 1), dtype=np.uint64, endpoint=True)
+    ks[0, 0:200] = 0  # bootstrap 0: 100 zero pairs its partner (1) does not have
+    ks[3, 1:O.n] = 0  # bootstrap 3: a single nonzero coefficient
+    luts = [[(3 * m + i) % 16 for m in range(16)] for i in range(count)]
+    got = pair.dev_blind_rotate(ks, luts)
+    assert (got == tp.dev_blind_rotate(ks, luts)).all()
+    for i in (0, 1, 3, count // 2, count - 1):
+        assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i

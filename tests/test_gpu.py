@@ -279,6 +279,31 @@ def test_metric_abc_256(gctx):
     assert got == 1 and st.ct_ops == 1523
 
 
+@pytest.mark.parametrize("hit", [True, False])
+def test_pair_shape_match_bit_identical(gctx, key_blob, monkeypatch, hit):
+    """/abc/ on 256 chars (its first level: 512 multi-value bootstraps) with the pair
+    shape on and off: the result ciphertext is the same bit for bit (multi-value and
+    sign jobs through both shapes)."""
+    p = gctx.params
+    if p.ring != F.RING_FFT or p.k != 1:
+        pytest.skip("the pair shape is the k = 1 latency geometry")
+    rng = np.random.default_rng(11)
+    s = _printable(rng, 256).replace("abc", "abd")
+    if hit:
+        s = s[:77] + "abc" + s[80:]
+    words = []
+    for lim in (0, 4096):
+        monkeypatch.setenv("FR_FFT_PAIR_BATCH", str(lim))
+        c = F.Context(device=0, params=F.default_params(k=p.k, N=p.N, ring=p.ring))
+        monkeypatch.delenv("FR_FFT_PAIR_BATCH")
+        c.load_client_key(key_blob)
+        c.gen_server_key(SEED)
+        o, _ = c.has_match(c.upload_radix(c.encrypt_str(s, seed=5)), "/abc/")
+        words.append(c.download_radix(o))
+        assert c.decrypt_radix(words[-1]) == int(hit)
+    assert (words[0] == words[1]).all()
+
+
 @pytest.mark.parametrize("kind", ["letters", "digit"])
 def test_config3_proxy(gctx, kind):
     rng = np.random.default_rng(4)
