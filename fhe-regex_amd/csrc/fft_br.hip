@@ -154,7 +154,9 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_LAT_PF2
 #define FR_LAT_PF2 2
 #endif
-// pair shape: the forward phase after which a step's third GGSW group loads
+// pair shape: the forward phase after which a step's third GGSW group loads (tools/ab_libs.sh,
+// profiles/r03/ab_pair_variants.log: after phase 0 / 1 / 2 / 3: 2.93 / 2.83 / 2.73 / 2.82 ms per
+// 512 bootstraps; the psi lookups moved ahead of the MAC barrier: 2.75, not kept)
 #ifndef FR_PAIR_LOAD
 #define FR_PAIR_LOAD 2
 #endif

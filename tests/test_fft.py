@@ -268,11 +268,13 @@ def test_fft_metric_config_256_chars(fctx):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("keygen", [F.KEYGEN_AUTO, F.KEYGEN_HOST])
-def test_fft_throughput_shape_bit_exact(key_blob, oracle_fft, point, keygen):
+def test_fft_throughput_shape_bit_exact(key_blob, oracle_fft, point, keygen, monkeypatch):
     """The throughput shape on a batch large enough for it (300 > the latency shape's
-    256), with the Fourier key laid out by the device keygen and by the host upload:
-    bit-exact against the oracle."""
+    256; k = 1 with the pair shape off), with the Fourier key laid out by the device
+    keygen and by the host upload: bit-exact against the oracle."""
+    monkeypatch.setenv("FR_FFT_PAIR_BATCH", "0")
     ctx = F.Context(device=0, params=F.default_params(k=point[0], N=point[1], ring=F.RING_FFT))
+    monkeypatch.delenv("FR_FFT_PAIR_BATCH")
     ctx.load_client_key(key_blob)
     ctx.set_keygen(keygen)
     ctx.gen_server_key(SEED)
