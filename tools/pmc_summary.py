@@ -6,7 +6,7 @@ MI355X_MICROARCH.md HBM section).  Launches are grouped by grid size; the
 per-match average over the blind-rotation launches of one has_match is what
 bench.py reports as roofline.traffic.
 The compute side: VALU wave-instructions (SQ_INSTS_VALU) per active-CU clock,
-active CUs = min(bootstraps, 256), clocks = GRBM_GUI_ACTIVE / 8 (the sum over the
+active CUs = min(workgroups, 256), clocks = GRBM_GUI_ACTIVE / 8 (the sum over the
 8 XCDs; MI355X_MICROARCH.md "DVFS give-back"), summed over the match's launches.
 The kernel source hash lets bench.py flag a summary of an older kernel as stale.
 Usage: python3 tools/pmc_summary.py PROFDIR OUT.json [k]
@@ -45,7 +45,11 @@ def main():
         f = fetch[key]["FETCH_SIZE"]
         w = write.get(key, {}).get("WRITE_SIZE", [0.0])
         wg = fetch[key]["_wg"][0]
-        ent = {"kernel": k, "grid": grid, "bootstraps": int(grid // wg), "calls": len(f),
+        # k_blind_rotate_fft<N, K, E, LAT, B>: B bootstraps per workgroup (the pair shape: 2)
+        targs = k.split("<")[1].rstrip(">").split(",") if "<" in k else []
+        per_wg = int(targs[4]) if "blind_rotate_fft" in k and len(targs) >= 5 else 1
+        ent = {"kernel": k, "grid": grid, "workgroups": int(grid // wg), "bootstraps": int(grid // wg) * per_wg,
+               "calls": len(f),
                "fetch_bytes": 2 * 1024 * sum(f) / len(f), "write_bytes": 1024 * sum(w) / len(w)}
         ent["hbm_bytes"] = ent["fetch_bytes"] + ent["write_bytes"]
         s = sq.get(key, {})
@@ -69,13 +73,13 @@ def main():
     per_launch = sum(e["hbm_bytes"] * e["calls"] for e in match) / max(1, sum(e["calls"] for e in match))
     ring = "fft" if any("blind_rotate_fft" in e.get("kernel", "") for e in launches) else "rns"
     valu = sum(e.get("valu_insts") or 0 for e in match)
-    cu_clk = sum(min(e["bootstraps"], 256) * e.get("grbm_gui_active_per_xcd", 0) for e in match)
+    cu_clk = sum(min(e["workgroups"], 256) * e.get("grbm_gui_active_per_xcd", 0) for e in match)
     src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
     res = {"hbm_bytes_per_launch": per_launch, "ring": ring, "k": int(sys.argv[3]) if len(sys.argv) > 3 else 1,
            "valu_per_cu_clk": valu / cu_clk if valu and cu_clk else None,
            "kernel_sha": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16],
            "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the match, averaged per "
-                   "launch; valu_per_cu_clk = sum SQ_INSTS_VALU / sum min(bootstraps, 256) GRBM_GUI_ACTIVE/8",
+                   "launch; valu_per_cu_clk = sum SQ_INSTS_VALU / sum min(workgroups, 256) GRBM_GUI_ACTIVE/8",
            "launches": launches}
     with open(out_path, "w") as f:
         json.dump(res, f, indent=1)
