@@ -510,6 +510,7 @@ def main():
     if args.saturate and rank == 0:
         src = [h for h in handles if h != F.NULL_CT]
         hs = [src[i % len(src)] for i in range(args.saturate)]
+        ctx.dev_bench_pbs(hs, 1)  # warm-up, as the latency probe below
         br_sat, tot_sat = ctx.dev_bench_pbs(hs, 2)
         kernel = {"gates_per_launch": args.saturate, "br_ms_per_launch": br_sat / 2,
                   "pbs_per_s": 2 * args.saturate / (tot_sat / 1e3),
