@@ -506,6 +506,22 @@ constexpr int fbr_threads() {
 // blocks, so it serves the N-entry and the N/2-entry (quadrant) table alike.
 __device__ __forceinline__ int psi_slot(int k) { return k ^ ((k >> 6) & 15) ^ ((k >> 5) & 1); }
 
+// Slot factor psi^(e (Lb + M sm)) = i^q psi^(e Lb), q = (e sm) mod 4 (fft::psi_quadrant of
+// the base): for odd sm, q is odd exactly when the uniform e is, so the swap of an odd turn is
+// one select per base shared by the slots sm = 1, 3, and every slot adds only a uniform sign
+// (i^q b = i^(q-1) (i b), q - 1 even).  The same values as psi_quadrant; 11 VALU per factor
+// over a lane's 4 slots instead of ~23 (latency step loop 602 -> 584 VALU per wave-step; one
+// bootstrap 1.355 -> 1.324 ms, 2048 10.00 -> 9.83 ms: profiles/r03/ab_slot_factor.log).
+// A 16-way uniform branch on (a_i, a_j) mod 4 that made every turn compile-time spilled
+// 14-84 VGPRs in every shape and was dropped.
+__device__ __forceinline__ void slot_factor(double br, double bi, uint32_t e, uint32_t sm, double& cr, double& ci) {
+    const uint32_t q = (e * sm) & 3u;
+    const bool swap = (sm & 1u) && (e & 1u);
+    const double ar = swap ? -bi : br, ai = swap ? br : bi;
+    const long long sg = (long long)((q >> 1) & 1u) << 63;
+    cr = __longlong_as_double(__double_as_longlong(ar) ^ sg);
+    ci = __longlong_as_double(__double_as_longlong(ai) ^ sg);
+}
 // twiddles in registers (latency shape, k = 1)
 template <int K, bool LAT>
 constexpr bool fbr_twr() {
@@ -892,8 +908,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                 double cr[3], ci[3];
 #pragma unroll
                 for (int h = 1; h < 3; ++h)  // uniform quarter turn
-                    fft::psi_quadrant(bre[b][h - 1][m >> 2], bim[b][h - 1][m >> 2], ((h == 1 ? ei[b] : ej[b]) * sm) & 3u,
-                                      cr[h], ci[h]);
+                    slot_factor(bre[b][h - 1][m >> 2], bim[b][h - 1][m >> 2], h == 1 ? ei[b] : ej[b], sm, cr[h], ci[h]);
 #ifdef FR_FFT_NOC0  // timing experiment only (wrong results): no pair-monomial product
                 cr[0] = cr[1] + cr[2], ci[0] = ci[1];
 #else
