@@ -483,8 +483,8 @@ constexpr int fbr_threads() {
 //  * latency, LAT (E = 4; launches of at most one bootstrap per CU): one
 //    workgroup per CU (k = 1: 8 waves; k = 2, N = 1024: 6 waves), 256 VGPRs; the
 //    step's 3 x (k+1) x E Fourier GGSW slots are loaded at the top of the step
-//    (they land during the digits and the forward FFT); the half psi^k table
-//    (k < N; psi^(k+N) = -psi^k) and two sets of exchange rows (forward + MAC /
+//    (they land during the digits and the forward FFT); the whole psi^k table
+//    (k < 2N: no sign flips on lookup) and two sets of exchange rows (forward + MAC /
 //    inverse: 3 barriers per step instead of 5) in LDS.  k = 1 keeps the lane's
 //    twiddles in registers (TWR); k = 2 reads them from LDS (the 36 GGSW values
 //    take the registers).
@@ -539,7 +539,7 @@ constexpr int fbr_twc_entries() {
 template <int N, int K, int E, bool LAT, int B = 1>
 constexpr size_t fbr_smem_bytes() {
     return 16 * ((LAT ? 2 : 1) * B * (K + 1) * (size_t)FGeo<N / 2, E>::NP + (B == 1 ? (size_t)N / 2 : 0) +
-                 (LAT && B == 1 ? (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
+                 (LAT && B == 1 ? 2 * (size_t)N : (size_t)N / 2) + (size_t)fbr_twc_entries<N, K, E, LAT>()) +
            B * (16 * MAX_OUT + 2 * 1026) + (B == 1 ? 4 * 17 * MAX_OUT : 0) + 2 * 514;
 }
 // workgroups per CU of the throughput shapes (LDS: fbr_smem_bytes * this <= 160 KB)
@@ -637,7 +637,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     double2* xbuf = fsm;                  // B x (K+1) rows of NP complex: bootstrap b, row P at b BS + P NP
     double2* ibuf = LAT ? xbuf + B * BS : xbuf;  // inverse-transform rows (latency shapes: separate)
     double2* tw = xbuf + (LAT ? 2 : 1) * B * BS;  // M forward twiddles (B = 1)
-    constexpr int NPSI = PSIQ ? N / 2 : N;
+    constexpr int NPSI = PSIQ ? N / 2 : 2 * N;  // (latency shape: the whole circle, no sign flips)
     double2* psi = tw + (B == 1 ? M : 0);  // psi^k, k < NPSI
     double2* twc = psi + NPSI;            // radix-4 products c ca (fbr_twc_entries)
     constexpr int NTWC = fbr_twc_entries<N, K, E, LAT>();
@@ -816,15 +816,14 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
                     for (int bb = 0; bb < NB; ++bb) {
                         const uint32_t k = __umul24(h == 0 ? ei[b] : ej[b], Lb[bb]) & (2 * N - 1);
-                        if constexpr (!PSIQ) {  // psi^(k+N) = -psi^k: flip both signs
+                        if constexpr (!PSIQ) {  // psi^k, k < 2N, straight from the table
 #ifdef FR_FFT_NOPSI  // timing experiment only (wrong results): no table lookups
                             const double2 c = make_double2((double)k, 0.5);
 #else
-                            const double2 c = psi[psi_slot((int)(k & (N - 1)))];
+                            const double2 c = psi[psi_slot((int)k)];
 #endif
-                            const long long sgn = (long long)((k >> (LOG2N2 - 1)) & 1) << 63;
-                            bre[b][h][bb] = __longlong_as_double(__double_as_longlong(c.x) ^ sgn);
-                            bim[b][h][bb] = __longlong_as_double(__double_as_longlong(c.y) ^ sgn);
+                            bre[b][h][bb] = c.x;
+                            bim[b][h][bb] = c.y;
                         } else {
                             const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
                             fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[b][h][bb], bim[b][h][bb]);
