@@ -13,5 +13,5 @@ for w in "config2 --params k2n1024" "config2" "metric --params k2n1024" "config3
   step 400 python3 bench.py --workload $w --steps 5 --warmup 2 --cpu-sample 0 --saturate 0 > "$out/bench_$tag.json" 2> "$out/bench_$tag.err" || { tail -20 "$out/bench_$tag.err"; exit 1; }
   python3 -c "
 import json; d=json.load(open('$out/bench_$tag.json'))
-print('$tag', d['config']['workload'], d['config']['params'], 'match_ms=%.2f'%d['match_ms'], 'rot=%d'%d['blind_rotations_per_match'], 'levels=%d'%d['levels'], 'value=%.0f'%d['value'], 'frac=%.3f'%d['roofline']['frac'], 'ok=%s'%(d['result_decrypted']==d['result_expected']))"
+print('$tag', d['config']['workload'], d['config']['params'], 'match_ms=%.2f'%d['match_ms'], 'rot=%d'%d['blind_rotations_per_step'], 'levels=%d'%d['levels'], 'value=%.0f'%d['value'], 'frac=%.3f'%d['roofline']['frac'], 'ok=%s'%(d['result_decrypted']==d['result_expected']))"
 done
