@@ -759,9 +759,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // single CU streams ~50 GB/s of key at 3.9 us per step); the others across the
     // step's own forward FFT.  The next unskipped step comes from the table nxt (no
     // control flow around the prefetch, which keeps it after the MAC's last use).
-    constexpr int NPF = LAT ? (K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;
+    constexpr int NPF = LAT ? (B > 1 ? 2 : K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;  // (pair shape: 2)
     constexpr bool LATPF = NPF > 0;
-    static_assert(B == 1 || NPF == 2, "pair shape: two groups a step ahead, the third in the forward FFT");
     // step t is skipped when every bootstrap's pair is (0, 0): X^0 acc - acc = 0.  The pair
     // shape runs a step that is zero for one bootstrap only: its factors c - 1 are exact
     // zeros, so its MAC output is 0 and the accumulate adds +-0.
