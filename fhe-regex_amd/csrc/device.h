@@ -123,12 +123,17 @@ class Device {
     void* take_event();
     void resolve_timers();
     void ensure_digits(size_t rows);
-    void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks);
-    void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n);
+    // ev_start / ev_stop (profiling): HIP events stamped by the kernels' own dispatch
+    // (hipExtLaunchKernel) -- the first kernel's start and the last one's end -- so timing
+    // adds no marker packets between dependent launches (each cost ~5 us of gap)
+    void launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks, void* ev_start = nullptr, void* ev_stop = nullptr);
+    void launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* ev_start = nullptr,
+                   void* ev_stop = nullptr);
     // FR_RING_FFT (fft.hip)
     void init_fft();
     void upload_fft_bsk(const std::vector<uint64_t>& bsk);
-    void launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream);
+    void launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream, void* ev_start = nullptr,
+                       void* ev_stop = nullptr);
     void free_fft();
     void build_ksk_limbs();  // d_kl_ from d_ksk_
     void stage_slot_list(const int* slots, size_t n);  // -> d_slot_list_ (stream order)
@@ -184,7 +189,7 @@ class Device {
     void* stage_ev_[2] = {nullptr, nullptr};
     int stage_ = 0;
     struct PendingTimer {
-        void* ev[3];
+        void* ev[4];  // KS start, KS end, BR start, BR end
         size_t gates, outs;
         bool lat, pair;
     };

@@ -20,6 +20,7 @@
 // negacyclic transform: forward Cooley-Tukey with zeta[k] = psi^brv(k),
 // outputs in bit-reversed slot order; inverse Gentleman-Sande with
 // psi^-brv(k) = -zeta[3*2^s - 1 - k] (negation folded into the butterfly).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1227,7 +1228,8 @@ void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uin
     HIP_CHECK(hipFree(coef));
 }
 
-void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
+void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks, void* ev_start, void* ev_stop) {
+    const hipEvent_t e0 = (hipEvent_t)ev_start, e1 = (hipEvent_t)ev_stop;
     if (ks_mfma_) {
         const int KD = p_.big() * p_.ks_level;
         if (KD % 256) throw Error(FR_ERR_INVALID, "MFMA keyswitch needs kN*ks_level % 256 == 0");
@@ -1235,8 +1237,9 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
         if (KD % 16) throw Error(FR_ERR_INVALID, "MFMA keyswitch: digit rows must be whole 16-byte vectors");
-        k_ks_digits<3, 5><<<dim3(8, (unsigned)bp), 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_cmap_,
-                                                                      p_.big(), d_dig_, d_ks, p_.n, p_.ks_stride());
+        hipExtLaunchKernelGGL(k_ks_digits<3, 5>, dim3(8, (unsigned)bp), dim3(256), 0, STREAM, e0, nullptr, 0, d_gates, (int)n,
+                              (const uint64_t*)d_arena_, p_.slot_stride(), (const int*)d_cmap_, p_.big(), d_dig_, d_ks,
+                              p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         // column tiles per wave: 1 (FR_KS_MC=2 shares each digit fragment between two; with
         // fragment-ordered operands that no longer pays: 512 gates 121 -> 103 us at 1)
@@ -1249,14 +1252,17 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
         if (ks_split_ > 0 && (KD / 256) % ks_split_ == 0) split = ks_split_;
         const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)((kl_cols_ + 128 * MC - 1) / (128 * MC)), (unsigned)split);
         if (MR == 4 && MC == 2)
-            k_ks_mfma<4, 2><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
-                                                      (unsigned long long*)d_ks, p_.ks_stride());
+            hipExtLaunchKernelGGL(k_ks_mfma<4, 2>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
+                                  (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
+                                  p_.ks_stride());
         else if (MR == 4)
-            k_ks_mfma<4, 1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
-                                                      (unsigned long long*)d_ks, p_.ks_stride());
+            hipExtLaunchKernelGGL(k_ks_mfma<4, 1>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
+                                  (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
+                                  p_.ks_stride());
         else
-            k_ks_mfma<1, 1><<<grid, 256, 0, STREAM>>>(d_dig_, d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
-                                                      (unsigned long long*)d_ks, p_.ks_stride());
+            hipExtLaunchKernelGGL(k_ks_mfma<1, 1>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
+                                  (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
+                                  p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         return;
     }
@@ -1270,25 +1276,28 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks) {
     splits = (chunks + per - 1) / per;
     if (splits > 1) HIP_CHECK(hipMemsetAsync(d_ks, 0, (size_t)8 * p_.ks_stride() * n, STREAM));
     dim3 grid((unsigned)btiles, (unsigned)ctiles, (unsigned)splits);
-    k_lincomb_keyswitch<3, 5><<<grid, 256, 0, STREAM>>>(d_gates, (int)n, d_arena_, p_.slot_stride(), d_cmap_, d_ksk_,
-                                                         p_.n, p_.big(), per, (unsigned long long*)d_ks, p_.ks_stride());
+    hipExtLaunchKernelGGL(k_lincomb_keyswitch<3, 5>, grid, dim3(256), 0, STREAM, e0, e1, 0, d_gates, (int)n,
+                          (const uint64_t*)d_arena_, p_.slot_stride(), (const int*)d_cmap_, (const uint64_t*)d_ksk_, p_.n,
+                          p_.big(), per, (unsigned long long*)d_ks, p_.ks_stride());
     HIP_CHECK(hipGetLastError());
 }
 
 bool Device::latency_shape(size_t n) const { return n <= (p_.ring == FR_RING_FFT ? fft_small_ : small_batch_); }
 bool Device::pair_shape(size_t n) const { return p_.ring == FR_RING_FFT && !latency_shape(n) && n <= fft_pair_; }
 
-void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n) {
+void Device::launch_br(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* ev_start, void* ev_stop) {
     if (p_.ring == FR_RING_FFT) {
-        launch_br_fft(d_gates, d_ks, n, stream_);
+        launch_br_fft(d_gates, d_ks, n, stream_, ev_start, ev_stop);
         return;
     }
     // small levels (at most one bootstrap per CU): more lanes per bootstrap for latency
     const int E = n <= small_batch_ ? e_small_ : e_;
     dispatch(p_, E, [&](auto n_, auto k_, auto e_c) {
         constexpr int N = decltype(n_)::value, K = decltype(k_)::value, E = decltype(e_c)::value;
-        k_blind_rotate<N, K, E><<<(unsigned)n, br_threads<N, K, E>(), br_smem_bytes<N, K, E>(), STREAM>>>(
-            d_ks, p_.ks_stride(), p_.n, d_gates, d_bsk_, d_tw_, d_arena_, p_.slot_stride());
+        hipExtLaunchKernelGGL(k_blind_rotate<N, K, E>, dim3((unsigned)n), dim3(br_threads<N, K, E>()),
+                              (uint32_t)br_smem_bytes<N, K, E>(), STREAM, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0,
+                              d_ks, p_.ks_stride(), p_.n, d_gates, (const uint32_t*)d_bsk_, (const uint32_t*)d_tw_,
+                              d_arena_, p_.slot_stride());
     });
     HIP_CHECK(hipGetLastError());
 }
@@ -1374,15 +1383,12 @@ void Device::free_gates(DevGate* d) {
 
 void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n) {
     PendingTimer t{};
-    if (profiling_) {
+    if (profiling_)
         for (auto& e : t.ev) e = take_event();
-        HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[0], STREAM));
-    }
-    launch_ks(d_gates, n, d_ks_);
-    if (profiling_) HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[1], STREAM));
-    launch_br(d_gates, d_ks_, n);
+    launch_ks(d_gates, n, d_ks_, t.ev[0], t.ev[1]);
+    launch_br(d_gates, d_ks_, n, t.ev[2], t.ev[3]);
+    HIP_CHECK(hipGetLastError());
     if (profiling_) {
-        HIP_CHECK(hipEventRecord((hipEvent_t)t.ev[2], STREAM));
         t.gates = n;
         t.lat = latency_shape(n);
         t.pair = pair_shape(n);
@@ -1424,7 +1430,7 @@ void Device::resolve_timers() {
     for (auto& t : pending_) {
         float ks = 0, br = 0;
         HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)t.ev[0], (hipEvent_t)t.ev[1]));
-        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[1], (hipEvent_t)t.ev[2]));
+        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[2], (hipEvent_t)t.ev[3]));
         timers_.ks_ms += ks;
         timers_.br_ms += br;
         timers_.br_launches += 1;

@@ -17,6 +17,7 @@
 // (coalesced [w][r][c][m][lane] layout) and their slot-wise monomial factors
 // psi^(e L) - 1 (quadrant table in LDS), inverse FFT, exact f64 -> torus
 // conversion and u64 accumulate.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 
 #include <cstring>
@@ -1128,7 +1129,8 @@ void Device::upload_fft_bsk(const std::vector<uint64_t>& bsk) {
     }
 }
 
-void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream) {
+void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t n, void* stream, void* ev_start,
+                           void* ev_stop) {
     const hipStream_t s = (hipStream_t)stream;
     fft_dispatch(p_, [&](auto nc, auto kc) {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
@@ -1137,10 +1139,11 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
             constexpr bool LAT = decltype(lat)::value;
             constexpr int B = decltype(bc)::value;
             if constexpr (fft_shape_ok<N, K, E>() && (B == 1 || K == 1))
-                k_blind_rotate_fft<N, K, E, LAT, B>
-                    <<<(unsigned)((n + B - 1) / B), fbr_threads<N, K, E>(), fbr_smem_bytes<N, K, E, LAT, B>(), s>>>(
-                        d_ks, p_.ks_stride(), p_.n, d_gates, (int)n, (const double2*)d_fbsk_[fbsk_index(E)],
-                        (const double2*)d_ftw_, (const double2*)d_fqt_, d_fleaf_, d_arena_, p_.slot_stride());
+                hipExtLaunchKernelGGL(k_blind_rotate_fft<N, K, E, LAT, B>, dim3((unsigned)((n + B - 1) / B)),
+                                      dim3(fbr_threads<N, K, E>()), (uint32_t)fbr_smem_bytes<N, K, E, LAT, B>(), s,
+                                      (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, d_ks, p_.ks_stride(), p_.n, d_gates,
+                                      (int)n, (const double2*)d_fbsk_[fbsk_index(E)], (const double2*)d_ftw_,
+                                      (const double2*)d_fqt_, (const uint16_t*)d_fleaf_, d_arena_, p_.slot_stride());
         };
         using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
