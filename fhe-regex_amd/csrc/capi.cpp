@@ -771,7 +771,8 @@ int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* lu
 int fr_set_profiling(fr_ctx* ctx, int32_t on) {
     FR_TRY({
         NEED(ctx);
-        ctx->device().set_profiling(on != 0);
+        if (on < 0 || on > 2) throw Error(FR_ERR_INVALID, "profiling level: 0, 1 or 2");
+        ctx->device().set_profiling(on);
     })
 }
 

@@ -96,7 +96,7 @@ class Device {
     void run_linear(const DevGate& g);
     void sync();
 
-    void set_profiling(bool on) { profiling_ = on; }
+    void set_profiling(int level) { profiling_ = level; }
     DeviceTimers& timers() { return timers_; }
 
     // single-stage entry points for parity tests
@@ -191,7 +191,7 @@ class Device {
     struct PendingTimer {
         void* ev[4];  // KS start, KS end, BR start, BR end
         size_t gates, outs;
-        bool lat, pair;
+        bool lat, pair, ks;
     };
     bool latency_shape(size_t n) const;  // launch_br's shape choice for n bootstraps
     bool pair_shape(size_t n) const;     // (FFT ring, k = 1: the pair shape)
@@ -199,7 +199,7 @@ class Device {
     std::vector<void*> event_pool_;
     uint64_t* d_ks_ = nullptr;
     size_t batch_cap_ = 0;
-    bool profiling_ = false;
+    int profiling_ = 0;  // fr_set_profiling level
     DeviceTimers timers_;
     void* ev_[4] = {nullptr, nullptr, nullptr, nullptr};
 };

@@ -1385,13 +1385,17 @@ void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n)
     PendingTimer t{};
     if (profiling_)
         for (auto& e : t.ev) e = take_event();
-    launch_ks(d_gates, n, d_ks_, t.ev[0], t.ev[1]);
+    // keyswitch events at level 2 only: two more event-stamped launches per level cost
+    // ~30 us per /abc/ match, the blind rotation's ~0 (tools/match_probe.py)
+    if (profiling_ >= 2) launch_ks(d_gates, n, d_ks_, t.ev[0], t.ev[1]);
+    else launch_ks(d_gates, n, d_ks_);
     launch_br(d_gates, d_ks_, n, t.ev[2], t.ev[3]);
     HIP_CHECK(hipGetLastError());
     if (profiling_) {
         t.gates = n;
         t.lat = latency_shape(n);
         t.pair = pair_shape(n);
+        t.ks = profiling_ >= 2;
         t.outs = 0;
         for (size_t i = 0; i < n; ++i) t.outs += host[i].n_out;
         pending_.push_back(t);
@@ -1429,7 +1433,7 @@ void* Device::take_event() {
 void Device::resolve_timers() {
     for (auto& t : pending_) {
         float ks = 0, br = 0;
-        HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)t.ev[0], (hipEvent_t)t.ev[1]));
+        if (t.ks) HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)t.ev[0], (hipEvent_t)t.ev[1]));
         HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[2], (hipEvent_t)t.ev[3]));
         timers_.ks_ms += ks;
         timers_.br_ms += br;

@@ -339,7 +339,8 @@ class Context:
         _check(lib().fr_plan_cache_stats(self.h, *[C.byref(x) for x in v]))
         return dict(zip(("entries", "slots", "hits", "misses"), (x.value for x in v)))
 
-    def set_profiling(self, on: bool):
+    def set_profiling(self, on):
+        """0/False off, 1/True blind-rotation timers, 2 also keyswitch timers (fr_set_profiling)."""
         _check(lib().fr_set_profiling(self.h, int(on)))
 
     # client side

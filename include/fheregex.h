@@ -233,7 +233,7 @@ int fr_plan_cache_stats(fr_ctx* ctx, uint64_t* entries, uint64_t* slots, uint64_
 int fr_export_bool_device(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst);
 int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct* out);
 /* Accumulated kernel timers of the profiling mode (fr_set_profiling): blind
- * rotation and keyswitch milliseconds, launches and bootstraps. */
+ * rotation and (level 2) keyswitch milliseconds, launches and bootstraps. */
 int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates);
 /* The part of those blind-rotation timers spent in latency-shape launches (at
  * most one bootstrap per CU: one workgroup per CU). */
@@ -341,7 +341,10 @@ int fr_set_lowering(fr_ctx* ctx, int32_t mode);
 /* Multi-value bootstrapping: gates of one level that read the same linear
  * combination share one blind rotation (default on). */
 int fr_set_multi_value(fr_ctx* ctx, int32_t on);
-/* Device profiling with HIP events around every launch (adds a sync per level). */
+/* Device profiling: 0 off; 1 blind-rotation timers (HIP events stamped by each blind
+ * rotation launch itself, hipExtLaunchKernel: no marker packets, no syncs; what bench.py's
+ * timed region uses); 2 also the keyswitch timers (two more stamped launches per level,
+ * ~30 us per /abc/ x 256 match).  Timers resolve at the next synchronisation. */
 int fr_set_profiling(fr_ctx* ctx, int32_t on);
 
 /* ----- single-stage device entry points (parity tests of each kernel) ----- */
