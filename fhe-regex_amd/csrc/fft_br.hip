@@ -161,6 +161,17 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_PAIR_LOAD
 #define FR_PAIR_LOAD 2
 #endif
+// pair shape A/B knobs: key groups loaded a step ahead (2; with 1 the third group loads after
+// forward phase FR_PAIR_LOAD2), and the inverse's c ca recomputed per phase (1) or kept (0)
+#ifndef FR_PAIR_PF
+#define FR_PAIR_PF 2
+#endif
+#ifndef FR_PAIR_LOAD2
+#define FR_PAIR_LOAD2 3
+#endif
+#ifndef FR_PAIR_CC
+#define FR_PAIR_CC 1
+#endif
 // latency shape, k = 1: the lane's twiddles in registers (1) or read from LDS (0)
 #ifndef FR_LAT_TWR
 #define FR_LAT_TWR 1
@@ -453,7 +464,7 @@ __device__ __forceinline__ void fforward_from(double2 (&x)[B][E], double2* row, 
 template <int M, int E, int p, bool NOPRE, bool TWR, int B, int BS, bool CARRY = false>
 __device__ __forceinline__ void finverse_from(double2 (&x)[B][E], double2* row, const FTwr<M, TWR ? E : 2>& twr,
                                               const double2* tw, const double2* twc, int tl) {
-    if constexpr (TWR && B > 1 && fradix4<M, E>()) {
+    if constexpr (TWR && B > 1 && fradix4<M, E>() && FR_PAIR_CC) {
         // pair shape: cc = c ca recomputed per phase (20 fewer live VGPRs; the same
         // fft::cmul as ftw_load_phase, so the same bits), shared by the B transforms
         const double2 c = twr.v[3 * p], ca = twr.v[3 * p + 1];
@@ -760,7 +771,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // single CU streams ~50 GB/s of key at 3.9 us per step); the others across the
     // step's own forward FFT.  The next unskipped step comes from the table nxt (no
     // control flow around the prefetch, which keeps it after the MAC's last use).
-    constexpr int NPF = LAT ? (B > 1 ? 2 : K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;  // (pair shape: 2)
+    constexpr int NPF = LAT ? (B > 1 ? FR_PAIR_PF : K == 1 ? FR_LAT_PF : FR_LAT_PF2) : 0;
     constexpr bool LATPF = NPF > 0;
     // step t is skipped when every bootstrap's pair is (0, 0): X^0 acc - acc = 0.  The pair
     // shape runs a step that is zero for one bootstrap only: its factors c - 1 are exact
@@ -794,8 +805,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // 64 live transform values leave no room for it across the whole transform).
         constexpr int G_TOP = !LAT || B > 1 ? 3 : (NPF < 2 || K == 1) ? NPF : 3;
         constexpr int G_L1 = !LAT ? 3 : B > 1 ? NPF : G_TOP + 1 < 3 ? G_TOP + 1 : 3;
-        constexpr int G_L2 = !LAT || B > 1 ? 3 : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
+        constexpr int G_L2 = !LAT ? 3 : B > 1 ? (NPF + 1 < 3 ? NPF + 1 : 3) : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
         constexpr int PH_L1 = B > 1 ? FR_PAIR_LOAD : FR_LAT_LOAD1;
+        constexpr int PH_L2 = B > 1 ? FR_PAIR_LOAD2 : FR_LAT_LOAD2;
         if constexpr (G_TOP < 3) {
             __builtin_amdgcn_sched_barrier(0);
             load_ggsw(G_TOP, t);
@@ -848,7 +860,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
                     load_ggsw(G_L1, t);
                     __builtin_amdgcn_sched_barrier(0);
                 }
-                if constexpr (p == FR_LAT_LOAD2 && G_L2 < 3) {
+                if constexpr (p == PH_L2 && G_L2 < 3) {
                     __builtin_amdgcn_sched_barrier(0);
                     load_ggsw(G_L2, t);
                     __builtin_amdgcn_sched_barrier(0);
