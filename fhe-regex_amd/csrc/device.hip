@@ -813,13 +813,31 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
             *(int4*)(dig + ks_frag(g, 16 * i, KT)) = int4{0, 0, 0, 0};
         return;
     }
-    const DevGate& gg = gates[g];
-    const int nin = gg.n_in;
+    // the gate's inputs resolved once per workgroup (16 lanes: descriptor word, content
+    // map), so every coefficient's input loads issue together instead of as a chain of
+    // descriptor -> map -> arena round trips per input
+    __shared__ int s_base[16];
+    __shared__ int s_w[16];
+    __shared__ int s_nin, s_off;
+    if (threadIdx.x < 16) {
+        const DevGate& gg = gates[g];
+        const int q = threadIdx.x, nin = gg.n_in;
+        s_base[q] = q < nin ? arena_slot(gg.in_slot[q], cmap) : 0;
+        s_w[q] = q < nin ? gg.in_w[q] : 0;
+        if (q == 0) s_nin = nin, s_off = gg.offset;
+    }
     for (int t = blockIdx.x * 256 + threadIdx.x; t < ks_n; t += gridDim.x * 256) ks[(size_t)g * ks_stride + t] = 0;
+    __syncthreads();
+    const int nin = s_nin;
     for (int i = blockIdx.x * 256 + threadIdx.x; i <= big; i += gridDim.x * 256) {
-        uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
-        for (int q = 0; q < nin; ++q)
-            v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + i];
+        uint64_t v = i == big ? (uint64_t)(int64_t)s_off << (DELTA_LOG - 1) : 0;
+        uint64_t xin[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < nin) xin[q] = arena[(size_t)s_base[q] * slot_stride + i];
+#pragma unroll
+        for (int q = 0; q < 16; ++q)
+            if (q < nin) v += (uint64_t)(int64_t)s_w[q] * xin[q];
         if (i == big) {
             ks[(size_t)g * ks_stride + ks_n] = v;  // column n of the output row; the MFMA pass subtracts
         } else {
@@ -832,21 +850,106 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
 }
 
 // one wave per MR x 1 tiles of 32 x 32 (gate, limb-column) and one K slice
-// (blockIdx.z of gridDim.z); 4 waves per workgroup along the column direction
+// (z of GZ); 4 waves per workgroup along the column direction
 // share the gate rows through L1, and the MR row tiles of a wave share each KSK
 // fragment (MR-fold less KSK traffic).  Partial results are subtracted from out
 // (pre-set to [t == n] * body) with 64-bit atomics: exact mod 2^64 in any order.
+// Workgroup order (one-dimensional grid, XCD-aware).  The hardware deals workgroup b to
+// XCD b % 8; XCD j takes the column groups [j GYX, (j+1) GYX) for every row group and
+// K slice, so each KSK limb fragment is fetched into one XCD's L2 only, and the row
+// groups of that XCD (dispatched next to each other: row group fastest) read it there.
+// Without the remap, the row groups of a column group sat on different XCDs and each
+// fetched the whole limb matrix (4x the KSK traffic at 512 gates).  xcd == 0: the plain
+// order (row group fastest, then column group, then K slice) for A/B runs.
+struct KsTile {
+    int x, y, z;
+};
+__device__ __forceinline__ bool ks_tile(int b, int GX, int GY, int GZ, int xcd, KsTile& t) {
+    if (!xcd) {
+        t.x = b % GX, t.y = (b / GX) % GY, t.z = b / (GX * GY);
+        return t.z < GZ;
+    }
+    const int GYX = (GY + 7) / 8, loc = b >> 3;
+    t.x = loc % GX;
+    t.z = (loc / GX) % GZ;
+    t.y = (b & 7) * GYX + loc / (GX * GZ);
+    return loc < GX * GZ * GYX && t.y < GY;
+}
+__host__ __device__ inline int ks_grid_blocks(int GX, int GY, int GZ, int xcd) {
+    return xcd ? 8 * GX * GZ * ((GY + 7) / 8) : GX * GY * GZ;
+}
+
+// k-steps per stage of the LDS-DMA ring of k_ks_glds
+#ifndef FR_KS_SK
+#define FR_KS_SK 2
+#endif
+// stages in the LDS-DMA ring of k_ks_glds (NB - 1 in flight)
+#ifndef FR_KS_NB
+#define FR_KS_NB 4
+#endif
+// (k_ks_mfma: k-steps in flight per wave, 8 with one row tile, 2 with four; four with four
+// row tiles took 512 gates from 100 to 158 us of keyswitch: the registers cost occupancy)
+// limb l of KSK column t sits at limb column 8 t + l (the MFMA's column operand), so the 8
+// limbs of a column land in 8 adjacent lanes of the accumulator.  (Measured and dropped in
+// round 3: the limbs as the row operand, each lane recombining two whole columns in
+// registers -- its atomics then scatter over 32 gate rows per instruction, 4x the memory-side
+// atomic transactions: 512 gates 73 -> 83 us.)
+__host__ __device__ inline int ks_limb_col(int t, int l) { return t * 8 + l; }
+// one MFMA step of a wave: acc += (32 digit rows) x (32 limb columns), k = 32
+__device__ __forceinline__ v16i_t ks_mma(v4i_t a, v4i_t b, v16i_t acc) {
+    return __builtin_amdgcn_mfma_i32_32x32x32_i8(a, b, acc, 0, 0, 0);
+}
+// a 64-bit value from another lane of the row by a DPP move (dpp_ctrl CTRL, all rows and banks)
+template <int CTRL>
+__device__ __forceinline__ uint64_t ks_dpp64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)v, CTRL, 0xF, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+// Epilogue: recombine the 8 byte limbs of each KSK column and subtract the wave's MR x MC
+// tiles from out (pre-set to [t == n] * body) with 64-bit atomics (exact mod 2^64 in any
+// order, so K slices meet there).  Rows g0 + 32 t, limb columns lcw + 32 c.
+template <int MR, int MC>
+__device__ __forceinline__ void ks_epilogue(const v16i_t (&acc)[MR][MC], int g0, int lcw, int r, int h, int B, int ncols,
+                                            int nlc, unsigned long long* __restrict__ out, int out_stride) {
+    // lane holds D[row][lc + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
+    // column (lc + r) / 8; the 8 limbs of a column meet across the lane's 8-lane group
+    const int limb = r & 7;
+#pragma unroll
+    for (int c = 0; c < MC; ++c) {
+        const int lc = lcw + 32 * c, col = (lc + r) >> 3;
+        if (lc >= nlc) continue;  // uniform
+#pragma unroll
+        for (int t = 0; t < MR; ++t)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                uint64_t v = (uint64_t)(int64_t)acc[t][c][i] << (8 * limb);
+                // sum over the 8 lanes of the column: DPP lane moves (quad_perm [1,0,3,2],
+                // [2,3,0,1], then row_half_mirror pairs the two quads of each 8-lane group)
+                v += ks_dpp64<0xB1>(v);
+                v += ks_dpp64<0x4E>(v);
+                v += ks_dpp64<0x141>(v);
+                const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (limb == 0 && g < B && col < ncols && v != 0)
+                    atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
+            }
+    }
+}
+
 template <int MR, int MC>
 __global__ void __launch_bounds__(256)
 k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, int KD, int ncols /* n + 1 */,
-          int nlc /* limb-columns, multiple of 32 */, unsigned long long* __restrict__ out, int out_stride) {
+          int nlc /* limb-columns, multiple of 32 */, unsigned long long* __restrict__ out, int out_stride, int GX,
+          int GY, int GZ, int xcd) {
     constexpr int UN = MR * MC == 1 ? 8 : 2;  // k-steps in flight per wave
+    KsTile tile;
+    if (!ks_tile((int)blockIdx.x, GX, GY, GZ, xcd, tile)) return;  // padding workgroup (uniform)
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int r = lane & 31, h = lane >> 5;
-    const int g0 = blockIdx.x * 32 * MR;
-    const int lcw = (blockIdx.y * 4 + w) * 32 * MC;  // first limb-column of this wave's MC column tiles
+    const int g0 = tile.x * 32 * MR;
+    const int lcw = (tile.y * 4 + w) * 32 * MC;  // first limb-column of this wave's MC column tiles
     if (lcw >= nlc) return;  // whole wave
-    const int kspan = KD / gridDim.z, kb = blockIdx.z * kspan, KT = KD / 32;
+    const int kspan = KD / GZ, kb = tile.z * kspan, KT = KD / 32;
     // fragment (tile, k) at ((tile * KT + k / 32) * 64 + lane) * 16: one k step of 32 is 1 KB
     const int8_t* ap = dig + ((size_t)(g0 >> 5) * KT * 64 + lane) * 16 + (size_t)kb * 32;
     const int8_t* bp[MC];
@@ -873,33 +976,101 @@ k_ks_mfma(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, 
             for (int t = 0; t < MR; ++t)
 #pragma unroll
                 for (int c = 0; c < MC; ++c)
-                    acc[t][c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(a[u][t], b[u][c], acc[t][c], 0, 0, 0);
+                    acc[t][c] = ks_mma(a[u][t], b[u][c], acc[t][c]);
     }
-    // lane holds D[row][lc + r] for rows (i&3) + 8(i>>2) + 4h: limb l = r & 7 of
-    // column (lc + r) / 8; sum the 8 limbs of a column across lanes r^1, r^2, r^4
-    const int limb = r & 7;
-#pragma unroll
-    for (int c = 0; c < MC; ++c) {
-        const int lc = lcw + 32 * c, col = (lc + r) >> 3;
-        if (lc >= nlc) continue;  // uniform
-#pragma unroll
-        for (int t = 0; t < MR; ++t)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                uint64_t v = (uint64_t)(int64_t)acc[t][c][i] << (8 * limb);
-#pragma unroll
-                for (int s = 1; s < 8; s <<= 1) {
-                    const uint32_t lo = __shfl_xor((uint32_t)v, s), hi = __shfl_xor((uint32_t)(v >> 32), s);
-                    v += ((uint64_t)hi << 32) | lo;
-                }
-                const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (limb == 0 && g < B && col < ncols && v != 0)
-                    atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
-            }
-    }
+    ks_epilogue<MR, MC>(acc, g0, lcw, r, h, B, ncols, nlc, out, out_stride);
 }
 
-// KSK (u64 [k][t], t <= n) -> balanced byte limbs, limb column t*8 + l, fragment order
+// Four-row-tile keyswitch with both operands staged by LDS-DMA (global_load_lds, 16 B per
+// lane, no VGPR staging) through a ring of NB stages of SK k-steps (round 3).  PMC at 512
+// gates of a register-staged version (digit tiles shared through LDS): 70 % of wave cycles
+// parked on memory waits, the MFMA pipes 16 % busy -- each wave kept only one or two k-steps
+// of fragments in flight against the HBM / L2 latency (more registers for more in flight
+// cost occupancy; sharing the digit tiles alone gained nothing).  Here
+// NB - 1 stages are in flight per workgroup at no register cost.  Wave w moves row tile w
+// of the digits and column tile w of the limbs; every wave reads the four digit tiles and
+// its own limb tile from the stage.  One raw barrier per stage, a counted vmcnt (never 0
+// in steady state) so the DMAs of later stages stay in flight across it.  512 / 254 gates:
+// keyswitch 98-100 -> 89-90 / 62-64 -> 55-57 us (tools/ks_probe.py; SK 1 / NB 8, SK 2 /
+// NB 5, SK 1 / NB 10 and 4, 8, 10 K slices all measured slower: profiles/r03/ab_ks_glds.log)
+template <int N>
+__device__ __forceinline__ void ks_wait_vm() {
+    static_assert(N >= 0 && N < 64, "vmcnt range");
+    // s_waitcnt simm16 (gfx9): vmcnt [3:0] + [15:14], expcnt [6:4] = 7, lgkmcnt [11:8] = 15 (no wait)
+    __builtin_amdgcn_s_waitcnt((N & 15) | (((N >> 4) & 3) << 14) | (7 << 4) | (15 << 8));
+}
+// wait until at most `after` stages of L DMAs each remain in flight (after <= A)
+template <int L, int A>
+__device__ __forceinline__ void ks_wait_after(int after) {
+    if constexpr (A > 0) {
+        if (after >= A) {
+            ks_wait_vm<A * L>();
+            return;
+        }
+        ks_wait_after<L, A - 1>(after);
+    } else {
+        ks_wait_vm<0>();
+    }
+}
+template <int SK, int NB>
+__global__ void __launch_bounds__(256)
+k_ks_glds(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, int KD, int ncols, int nlc,
+          unsigned long long* __restrict__ out, int out_stride, int GX, int GY, int GZ, int xcd) {
+    constexpr int MR = 4, L = 2 * SK;  // DMAs per wave per stage
+    static_assert(NB >= 2 && (NB - 2) * 2 * SK < 64, "ring depth");
+    __shared__ v4i_t ring[NB][2][4][SK][64];  // [stage][digits, limbs][tile][k-step][lane]
+    KsTile tile;
+    if (!ks_tile((int)blockIdx.x, GX, GY, GZ, xcd, tile)) return;  // padding workgroup (uniform)
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int r = lane & 31, h = lane >> 5;
+    const int g0 = tile.x * 32 * MR;
+    const int lcw = (tile.y * 4 + w) * 32;  // this wave's limb-column tile (past nlc: computed, dropped)
+    const int kspan = KD / GZ, kb = tile.z * kspan, KT = KD / 32;
+    const int8_t* ap = dig + ((size_t)((g0 >> 5) + w) * KT * 64 + lane) * 16 + (size_t)kb * 32;
+    const int8_t* bp = kl + ((size_t)(min(lcw, nlc - 32) >> 5) * KT * 64 + lane) * 16 + (size_t)kb * 32;
+    const int S = kspan / (32 * SK);  // kspan is a multiple of 256 (host)
+    auto issue = [&](int st) {
+        const int buf = st % NB;
+#pragma unroll
+        for (int u = 0; u < SK; ++u) {
+            const size_t off = (size_t)(st * SK + u) * 32 * 32;
+            __builtin_amdgcn_global_load_lds((const void*)(ap + off),
+                                             (__attribute__((address_space(3))) void*)&ring[buf][0][w][u][0], 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(bp + off),
+                                             (__attribute__((address_space(3))) void*)&ring[buf][1][w][u][0], 16, 0, 0);
+        }
+    };
+    v16i_t acc[MR][1];
+#pragma unroll
+    for (int t = 0; t < MR; ++t) acc[t][0] = v16i_t{0};
+#pragma unroll
+    for (int st = 0; st < NB - 1; ++st)
+        if (st < S) issue(st);
+    for (int s = 0; s < S; ++s) {
+        // this wave's DMAs of stage s have landed once at most those of the stages after it remain
+        ks_wait_after<L, NB - 2>(min(NB - 2, S - 1 - s));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every wave's stage s landed; stage s - 1's buffer read by all
+        asm volatile("" ::: "memory");
+        if (s + NB - 1 < S) issue(s + NB - 1);  // into stage s - 1's buffer
+        const int cur = s % NB;
+        v4i_t a[SK][MR], b[SK];
+#pragma unroll
+        for (int u = 0; u < SK; ++u) {
+            b[u] = ring[cur][1][w][u][lane];
+#pragma unroll
+            for (int t = 0; t < MR; ++t) a[u][t] = ring[cur][0][t][u][lane];
+        }
+#pragma unroll
+        for (int u = 0; u < SK; ++u)
+#pragma unroll
+            for (int t = 0; t < MR; ++t) acc[t][0] = ks_mma(a[u][t], b[u], acc[t][0]);
+    }
+    if (lcw < nlc) ks_epilogue<MR, 1>(acc, g0, lcw, r, h, B, ncols, nlc, out, out_stride);
+}
+
+// KSK (u64 [k][t], t <= n) -> balanced byte limbs in fragment order, limb l of column t at
+// limb column ks_limb_col(t, l)
 __global__ void __launch_bounds__(256) k_ksk_limbs(const uint64_t* __restrict__ ksk, int KD, int ncols, int nlc,
                                                    int8_t* __restrict__ kl) {
     const int KT = KD / 32;
@@ -915,7 +1086,8 @@ __global__ void __launch_bounds__(256) k_ksk_limbs(const uint64_t* __restrict__ 
             v -= 256;
             x += 1;
         }
-        if (t * 8 + l < nlc) kl[ks_frag(t * 8 + l, k, KT)] = (int8_t)v;
+        const int lc = ks_limb_col(t, l);
+        if (lc < nlc) kl[ks_frag(lc, k, KT)] = (int8_t)v;
     }
 }
 
@@ -1002,6 +1174,8 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_KS_MR4_MIN")) ks_mr4_min_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_KS_MC")) ks_mc_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_KS_SPLIT")) ks_split_ = std::atoi(ev);
+    if (const char* ev = std::getenv("FR_KS_XCD")) ks_xcd_ = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("FR_KS_LDS")) ks_lds_ = std::atoi(ev) != 0;
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -1250,19 +1424,24 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks, void* e
         int split = MR == 1 ? 8 : 5;
         while ((KD / 256) % split) --split;
         if (ks_split_ > 0 && (KD / 256) % ks_split_ == 0) split = ks_split_;
-        const dim3 grid((unsigned)(bp / (32 * MR)), (unsigned)((kl_cols_ + 128 * MC - 1) / (128 * MC)), (unsigned)split);
-        if (MR == 4 && MC == 2)
+        const int GX = (int)(bp / (32 * MR)), GY = (kl_cols_ + 128 * MC - 1) / (128 * MC), GZ = split;
+        const dim3 grid((unsigned)ks_grid_blocks(GX, GY, GZ, ks_xcd_));
+        if (MR == 4 && MC == 1 && ks_lds_)
+            hipExtLaunchKernelGGL(k_ks_glds<FR_KS_SK, FR_KS_NB>, grid, dim3(256), 0, STREAM, nullptr, e1, 0,
+                                  (const int8_t*)d_dig_, (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_,
+                                  (unsigned long long*)d_ks, p_.ks_stride(), GX, GY, GZ, ks_xcd_);
+        else if (MR == 4 && MC == 2)
             hipExtLaunchKernelGGL(k_ks_mfma<4, 2>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
                                   (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
-                                  p_.ks_stride());
+                                  p_.ks_stride(), GX, GY, GZ, ks_xcd_);
         else if (MR == 4)
             hipExtLaunchKernelGGL(k_ks_mfma<4, 1>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
                                   (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
-                                  p_.ks_stride());
+                                  p_.ks_stride(), GX, GY, GZ, ks_xcd_);
         else
             hipExtLaunchKernelGGL(k_ks_mfma<1, 1>, grid, dim3(256), 0, STREAM, nullptr, e1, 0, (const int8_t*)d_dig_,
                                   (const int8_t*)d_kl_, (int)n, KD, p_.n + 1, kl_cols_, (unsigned long long*)d_ks,
-                                  p_.ks_stride());
+                                  p_.ks_stride(), GX, GY, GZ, ks_xcd_);
         HIP_CHECK(hipGetLastError());
         return;
     }

@@ -107,6 +107,21 @@ def test_keyswitch_two_column_tiles_bit_exact(key_blob, fixture_key, monkeypatch
     assert (ctx.dev_keyswitch(blocks) == O.keyswitch(blocks)).all()
 
 
+@pytest.mark.parametrize("count", [1, 17, 600])
+def test_keyswitch_plain_workgroup_order_bit_exact(key_blob, fixture_key, monkeypatch, count):
+    """The keyswitch GEMM's plain workgroup order (FR_KS_XCD=0; the default deals
+    column groups to XCDs) gives the oracle's words too, with one and four row tiles
+    per wave."""
+    monkeypatch.setenv("FR_KS_XCD", "0")
+    ctx = F.Context(device=0)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    O = of.Oracle(fixture_key, seed=SEED)
+    rng = np.random.default_rng(count + 1)
+    blocks = rng.integers(0, 2**64 - 1, (count, ctx.lwe_len), dtype=np.uint64, endpoint=True)
+    assert (ctx.dev_keyswitch(blocks) == O.keyswitch(blocks)).all()
+
+
 def test_blind_rotate_bit_exact(gctx, oracle_k1):
     O = oracle_k1
     blocks = O.encrypt_blocks([5, 12, 0], seed=31)

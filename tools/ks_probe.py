@@ -27,4 +27,6 @@ for cnt in sizes:
         ks.append((tot - br) * 1e3)
     out[cnt] = round(statistics.median(ks), 1)
 env = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("FR_KS"))
+if os.environ.get("FHEREGEX_LIB"):
+    env = (env + " lib=" + os.path.basename(os.environ["FHEREGEX_LIB"])).strip()
 print(env or "default", "ks_us", out, flush=True)
