@@ -813,31 +813,13 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
             *(int4*)(dig + ks_frag(g, 16 * i, KT)) = int4{0, 0, 0, 0};
         return;
     }
-    // the gate's inputs resolved once per workgroup (16 lanes: descriptor word, content
-    // map), so every coefficient's input loads issue together instead of as a chain of
-    // descriptor -> map -> arena round trips per input
-    __shared__ int s_base[16];
-    __shared__ int s_w[16];
-    __shared__ int s_nin, s_off;
-    if (threadIdx.x < 16) {
-        const DevGate& gg = gates[g];
-        const int q = threadIdx.x, nin = gg.n_in;
-        s_base[q] = q < nin ? arena_slot(gg.in_slot[q], cmap) : 0;
-        s_w[q] = q < nin ? gg.in_w[q] : 0;
-        if (q == 0) s_nin = nin, s_off = gg.offset;
-    }
+    const DevGate& gg = gates[g];
+    const int nin = gg.n_in;
     for (int t = blockIdx.x * 256 + threadIdx.x; t < ks_n; t += gridDim.x * 256) ks[(size_t)g * ks_stride + t] = 0;
-    __syncthreads();
-    const int nin = s_nin;
     for (int i = blockIdx.x * 256 + threadIdx.x; i <= big; i += gridDim.x * 256) {
-        uint64_t v = i == big ? (uint64_t)(int64_t)s_off << (DELTA_LOG - 1) : 0;
-        uint64_t xin[16];
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if (q < nin) xin[q] = arena[(size_t)s_base[q] * slot_stride + i];
-#pragma unroll
-        for (int q = 0; q < 16; ++q)
-            if (q < nin) v += (uint64_t)(int64_t)s_w[q] * xin[q];
+        uint64_t v = i == big ? (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1) : 0;
+        for (int q = 0; q < nin; ++q)
+            v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + i];
         if (i == big) {
             ks[(size_t)g * ks_stride + ks_n] = v;  // column n of the output row; the MFMA pass subtracts
         } else {
@@ -906,6 +888,7 @@ __device__ __forceinline__ uint64_t ks_dpp64(uint64_t v) {
     const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(v >> 32), CTRL, 0xF, 0xF, false);
     return ((uint64_t)hi << 32) | lo;
 }
+__device__ __forceinline__ bool lane_is_zero(int r, int h) { return r == 0 && h == 0; }
 // Epilogue: recombine the 8 byte limbs of each KSK column and subtract the wave's MR x MC
 // tiles from out (pre-set to [t == n] * body) with 64-bit atomics (exact mod 2^64 in any
 // order, so K slices meet there).  Rows g0 + 32 t, limb columns lcw + 32 c.
@@ -930,8 +913,15 @@ __device__ __forceinline__ void ks_epilogue(const v16i_t (&acc)[MR][MC], int g0,
                 v += ks_dpp64<0x4E>(v);
                 v += ks_dpp64<0x141>(v);
                 const int g = g0 + 32 * t + (i & 3) + 8 * (i >> 2) + 4 * h;
+#if defined(FR_KS_TIMING_STORE)  // timing experiment only (wrong results with K slices): plain stores
+                if (limb == 0 && g < B && col < ncols) out[(size_t)g * out_stride + col] = 0 - v;
+#elif defined(FR_KS_TIMING_NOEPI)  // timing experiment only: one store per wave instead of the epilogue
+                if (i == 0 && t == 0 && c == 0 && lane_is_zero(r, h)) out[(size_t)g0 * out_stride] = v;
+                continue;
+#else
                 if (limb == 0 && g < B && col < ncols && v != 0)
                     atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
+#endif
             }
     }
 }
@@ -1066,7 +1056,29 @@ k_ks_glds(const int8_t* __restrict__ dig, const int8_t* __restrict__ kl, int B, 
 #pragma unroll
             for (int t = 0; t < MR; ++t) acc[t][0] = ks_mma(a[u][t], b[u], acc[t][0]);
     }
-    if (lcw < nlc) ks_epilogue<MR, 1>(acc, g0, lcw, r, h, B, ncols, nlc, out, out_stride);
+    // Epilogue through LDS (the ring is free once every wave has passed the last stage): wave w
+    // stores its 128 x 32 tile of i32 limb sums row-major ([row][limb column], 128 B rows,
+    // conflict-free b32 stores), then lane L reads KSK column L & 3 of rows (L >> 2) + 16 j,
+    // its 8 limbs as two b128 reads, recombines them in registers and subtracts the column with
+    // one atomic: 8 atomics per lane, 16 rows x 4 adjacent columns per instruction (against 64
+    // values x three 64-bit DPP rounds per lane in ks_epilogue)
+    __syncthreads();
+    if (lcw >= nlc) return;  // whole wave (no barrier below)
+    int* tl = (int*)&ring[0][0][0][0][0] + w * 128 * 32;
+#pragma unroll
+    for (int t = 0; t < MR; ++t)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) tl[(32 * t + (i & 3) + 8 * (i >> 2) + 4 * h) * 32 + r] = acc[t][0][i];
+    const int c = lane & 3, col = (lcw >> 3) + c;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int row = (lane >> 2) + 16 * j, g = g0 + row;
+        const v4i_t lo = *(const v4i_t*)(tl + row * 32 + 8 * c), hi = *(const v4i_t*)(tl + row * 32 + 8 * c + 4);
+        uint64_t v = 0;
+#pragma unroll
+        for (int l = 0; l < 4; ++l) v += ((uint64_t)(int64_t)lo[l] << (8 * l)) + ((uint64_t)(int64_t)hi[l] << (8 * l + 32));
+        if (g < B && col < ncols && v != 0) atomicAdd(&out[(size_t)g * out_stride + col], (unsigned long long)(0 - v));
+    }
 }
 
 // KSK (u64 [k][t], t <= n) -> balanced byte limbs in fragment order, limb l of column t at
@@ -1418,13 +1430,16 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks, void* e
         // column tiles per wave: 1 (FR_KS_MC=2 shares each digit fragment between two; with
         // fragment-ordered operands that no longer pays: 512 gates 121 -> 103 us at 1)
         const int MC = MR == 4 && ks_mc_ == 2 ? 2 : 1;
-        // K slices (partial sums meet in 64-bit atomics, so more slices cost atomic traffic):
-        // 8 for one row tile per wave, 5 for four (tools/ks_sweep.sh: 1-17 gates ~31 us,
-        // 254 gates 75 -> 61 us against 8); a divisor of KD / 256
-        int split = MR == 1 ? 8 : 5;
+        // K slices (partial sums meet in 64-bit atomics, so more slices cost atomic traffic, and
+        // every slice its epilogue): 8 for one row tile per wave (1-17 gates ~30 us); four row
+        // tiles (k_ks_glds): 5 up to 256 gates, 2 up to 512, then 1 (profiles/r03/ab_ks_glds.log:
+        // 254 gates 55 us at 4-5 against 60 at 2; 512: 77 at 2 against 86-89 at 4-5; 1024 /
+        // 2048: 125 / 231 at 1 against 130 / 234 at 2); a divisor of KD / 256
+        const int gx = (int)(bp / (32 * MR));
+        int split = MR == 1 ? 8 : gx <= 2 ? 5 : gx <= 4 ? 2 : 1;
         while ((KD / 256) % split) --split;
         if (ks_split_ > 0 && (KD / 256) % ks_split_ == 0) split = ks_split_;
-        const int GX = (int)(bp / (32 * MR)), GY = (kl_cols_ + 128 * MC - 1) / (128 * MC), GZ = split;
+        const int GX = gx, GY = (kl_cols_ + 128 * MC - 1) / (128 * MC), GZ = split;
         const dim3 grid((unsigned)ks_grid_blocks(GX, GY, GZ, ks_xcd_));
         if (MR == 4 && MC == 1 && ks_lds_)
             hipExtLaunchKernelGGL(k_ks_glds<FR_KS_SK, FR_KS_NB>, grid, dim3(256), 0, STREAM, nullptr, e1, 0,

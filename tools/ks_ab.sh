@@ -13,7 +13,7 @@ tail -1 "$out/tests.log"
 for r in $(seq "$rounds"); do
   for e in "$@"; do
     [ "$e" = default ] && e=""
-    env $e timeout -k 10 120 python3 tools/ks_probe.py 9 1 17 254 512 >> "$out/ks_ab.log" 2>&1 || { cat "$out/ks_ab.log"; exit 1; }
+    env $e timeout -k 10 120 python3 tools/ks_probe.py 9 ${KS_SIZES:-1 17 254 512} >> "$out/ks_ab.log" 2>&1 || { cat "$out/ks_ab.log"; exit 1; }
   done
 done
 cat "$out/ks_ab.log"
