@@ -162,6 +162,7 @@ class Device {
     int ks_mc_ = 0;               // FR_KS_MC=2: two column tiles per wave in the 4-row-tile shape (else one)
     int ks_split_ = 0;            // FR_KS_SPLIT: K slices (a divisor of kN*ks_level/256; 0: auto)
     int ks_xcd_ = 1;              // FR_KS_XCD=0: plain workgroup order of the MFMA keyswitch (k_ks_mfma)
+    bool ks_dig16_ = true;        // FR_KS_DIG16=0: the digit pass with byte stores (k_ks_digits)
     bool ks_lds_ = true;          // FR_KS_LDS=0: four-row-tile keyswitch without the LDS-DMA ring (k_ks_mfma<4, 1>)
     int8_t* d_dig_ = nullptr;     // keyswitch digits [rows][kN*ks_level]
     size_t dig_cap_ = 0;

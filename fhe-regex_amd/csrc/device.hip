@@ -831,6 +831,67 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
     }
 }
 
+// The same pass, one workgroup per gate and sixteen consecutive coefficients per thread: its
+// 16 KSL digits are KSL whole 16-byte pieces of the fragment-ordered digit row (k = 16 KSL q ..
+// 16 KSL q + 16 KSL - 1 starts a piece), stored as 16-byte writes, where k_ks_digits's byte
+// stores scatter every digit over 16-byte pieces of 10 fragments; the inputs load as 16-byte
+// vectors.  (needs big % 16 == 0; the body coefficient by thread 0)
+template <int KSB, int KSL>
+__global__ void __launch_bounds__(128)
+k_ks_digits16(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
+              const int* __restrict__ cmap, int big, int8_t* __restrict__ dig, uint64_t* __restrict__ ks, int ks_n,
+              int ks_stride) {
+    const int g = blockIdx.x, KT = big * KSL / 32, groups = big / 16;
+    if (g >= B) {  // padding row of the last row tile: zero digits
+        for (int q = threadIdx.x; q < groups; q += blockDim.x)
+#pragma unroll
+            for (int c = 0; c < KSL; ++c) *(int4*)(dig + ks_frag(g, 16 * (q * KSL + c), KT)) = int4{0, 0, 0, 0};
+        return;
+    }
+    const DevGate& gg = gates[g];
+    const int nin = gg.n_in;
+    for (int t = threadIdx.x; t < ks_n; t += blockDim.x) ks[(size_t)g * ks_stride + t] = 0;
+    if (threadIdx.x == 0) {  // column n of the output row (the body); the MFMA pass subtracts
+        uint64_t v = (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1);
+        for (int q = 0; q < nin; ++q)
+            v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + big];
+        ks[(size_t)g * ks_stride + ks_n] = v;
+    }
+    for (int q = threadIdx.x; q < groups; q += blockDim.x) {
+        uint64_t v[16];
+#pragma unroll
+        for (int e = 0; e < 16; ++e) v[e] = 0;
+        for (int qi = 0; qi < nin; ++qi) {
+            const uint64_t w = (uint64_t)(int64_t)gg.in_w[qi];
+            const ulonglong2* src =
+                (const ulonglong2*)(arena + (size_t)arena_slot(gg.in_slot[qi], cmap) * slot_stride + 16 * q);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+                const ulonglong2 x = src[e];
+                v[2 * e] += w * x.x;
+                v[2 * e + 1] += w * x.y;
+            }
+        }
+        uint32_t words[4 * KSL];
+#pragma unroll
+        for (int b = 0; b < 4 * KSL; ++b) words[b] = 0;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+            int32_t d[KSL];
+            ks_decompose<KSB, KSL>(v[e], d);
+#pragma unroll
+            for (int j = 0; j < KSL; ++j) {
+                const int byte = e * KSL + j;
+                words[byte >> 2] |= (uint32_t)(uint8_t)(int8_t)d[j] << (8 * (byte & 3));
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < KSL; ++c)
+            *(uint4*)(dig + ks_frag(g, 16 * (q * KSL + c), KT)) =
+                uint4{words[4 * c], words[4 * c + 1], words[4 * c + 2], words[4 * c + 3]};
+    }
+}
+
 // one wave per MR x 1 tiles of 32 x 32 (gate, limb-column) and one K slice
 // (z of GZ); 4 waves per workgroup along the column direction
 // share the gate rows through L1, and the MR row tiles of a wave share each KSK
@@ -1188,6 +1249,7 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_KS_SPLIT")) ks_split_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_KS_XCD")) ks_xcd_ = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("FR_KS_LDS")) ks_lds_ = std::atoi(ev) != 0;
+    if (const char* ev = std::getenv("FR_KS_DIG16")) ks_dig16_ = std::atoi(ev) != 0;
     if ((e_ != 8 && e_ != 16) || (e_small_ != 8 && e_small_ != 16))
         throw Error(FR_ERR_INVALID, "FR_LANE_ELEMS / FR_SMALL_LANE_ELEMS must be 8 or 16");
     for (int e : {8, 16})
@@ -1423,9 +1485,14 @@ void Device::launch_ks(const DevGate* d_gates, size_t n, uint64_t* d_ks, void* e
         const size_t bp = (n + 32 * MR - 1) / (32 * MR) * (32 * MR);
         ensure_digits(bp);
         if (KD % 16) throw Error(FR_ERR_INVALID, "MFMA keyswitch: digit rows must be whole 16-byte vectors");
-        hipExtLaunchKernelGGL(k_ks_digits<3, 5>, dim3(8, (unsigned)bp), dim3(256), 0, STREAM, e0, nullptr, 0, d_gates, (int)n,
-                              (const uint64_t*)d_arena_, p_.slot_stride(), (const int*)d_cmap_, p_.big(), d_dig_, d_ks,
-                              p_.n, p_.ks_stride());
+        if (ks_dig16_ && p_.big() % 16 == 0)
+            hipExtLaunchKernelGGL(k_ks_digits16<3, 5>, dim3((unsigned)bp), dim3(128), 0, STREAM, e0, nullptr, 0, d_gates,
+                                  (int)n, (const uint64_t*)d_arena_, p_.slot_stride(), (const int*)d_cmap_, p_.big(),
+                                  d_dig_, d_ks, p_.n, p_.ks_stride());
+        else
+            hipExtLaunchKernelGGL(k_ks_digits<3, 5>, dim3(8, (unsigned)bp), dim3(256), 0, STREAM, e0, nullptr, 0, d_gates,
+                                  (int)n, (const uint64_t*)d_arena_, p_.slot_stride(), (const int*)d_cmap_, p_.big(),
+                                  d_dig_, d_ks, p_.n, p_.ks_stride());
         HIP_CHECK(hipGetLastError());
         // column tiles per wave: 1 (FR_KS_MC=2 shares each digit fragment between two; with
         // fragment-ordered operands that no longer pays: 512 gates 121 -> 103 us at 1)

@@ -107,6 +107,19 @@ def test_keyswitch_two_column_tiles_bit_exact(key_blob, fixture_key, monkeypatch
     assert (ctx.dev_keyswitch(blocks) == O.keyswitch(blocks)).all()
 
 
+def test_keyswitch_byte_store_digit_pass_bit_exact(key_blob, fixture_key, monkeypatch):
+    """The digit pass with per-digit byte stores (FR_KS_DIG16=0; the default writes each
+    thread's 16 coefficients as whole 16-byte fragment pieces) gives the oracle's words."""
+    monkeypatch.setenv("FR_KS_DIG16", "0")
+    ctx = F.Context(device=0)
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    O = of.Oracle(fixture_key, seed=SEED)
+    rng = np.random.default_rng(300)
+    blocks = rng.integers(0, 2**64 - 1, (300, ctx.lwe_len), dtype=np.uint64, endpoint=True)
+    assert (ctx.dev_keyswitch(blocks) == O.keyswitch(blocks)).all()
+
+
 @pytest.mark.parametrize("count", [1, 17, 600])
 def test_keyswitch_plain_workgroup_order_bit_exact(key_blob, fixture_key, monkeypatch, count):
     """The keyswitch GEMM's plain workgroup order (FR_KS_XCD=0; the default deals
