@@ -166,6 +166,21 @@ class Merged {
             default: return false;
         }
     }
+    static bool has_anchor(const Re& re) {
+        switch (re.kind) {
+            case Re::SOF:
+            case Re::EOF_: return true;
+            case Re::SEQ:
+                for (auto& x : re.xs)
+                    if (has_anchor(*x)) return true;
+                return false;
+            case Re::EITHER: return has_anchor(*re.a) || has_anchor(*re.b);
+            case Re::OPTIONAL:
+            case Re::REPEATED:
+            case Re::NOT: return re.a && has_anchor(*re.a);
+            default: return false;
+        }
+    }
     static bool nullable_or_anchor(const Re& re) {
         switch (re.kind) {
             case Re::SOF:
@@ -256,11 +271,25 @@ class Merged {
         }
         // unbounded: at_most = L - p.  Exact as an unbounded closure when the
         // operand consumes at least one char per repetition (no path can then
-        // reach more than L - p repetitions).
-        if (nullable_or_anchor(*re.a))
-            throw Error(FR_ERR_INVALID, "merged engine: unbounded repetition of a nullable operand");
-        if (lo == 0) merge(out, r);
-        Reach lev = r;
+        // reach more than L - p repetitions).  A nullable operand without anchors
+        // (round 3) can also repeat empty, at every position below L and with no
+        // condition: a position q reached by k <= q - p non-empty repetitions is
+        // reached within the reference's counts [max(1,lo), L - p] (lo = 0: up to
+        // L - p + 1) by padding with empty ones, as long as the count range of the
+        // entry position p is not empty: lo <= L - p.  So the closure stays exact
+        // once entries with L - p < lo are dropped (engine.rs:127-183 enumerates
+        // nothing there).  An operand holding an anchor matches empty only at 0 or
+        // L and stays refused.
+        Reach rin = r;
+        if (nullable_or_anchor(*re.a)) {
+            if (has_anchor(*re.a))
+                throw Error(FR_ERR_INVALID,
+                            "merged engine: unbounded repetition of a nullable operand holding an anchor");
+            for (size_t p = 0; p <= L_; ++p)
+                if (L_ - p < lo) rin[p] = ABSENT;
+        }
+        if (lo == 0) merge(out, rin);
+        Reach lev = rin;
         const uint64_t first = std::max<uint64_t>(1, lo);
         for (uint64_t k = 1; k <= first; ++k) {
             lev = apply(*re.a, lev);

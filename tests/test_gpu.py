@@ -709,6 +709,22 @@ def test_fuzz_scale_vs_oracle(gctx):
             gctx.release(h)
 
 
+def test_fuzz_boundary_vs_oracle(gctx):
+    """30 seeded random patterns on 256-512 encrypted chars with a matching string, or a
+    one-character near miss of it, planted at the first or the last start offsets
+    (tests/golden/fuzz_boundary.json, made by make_fuzz_boundary.py from the oracle's
+    position-set simulator; 22 match, 8 do not): start-offset and anchor boundaries
+    (engine.rs:15-18, 51-57) on full-size random circuits, each decrypted result against
+    the oracle's."""
+    cases = load("fuzz_boundary.json")["cases"]
+    for i, cse in enumerate(cases):
+        hs = gctx.encrypt_upload_str(cse["content"], seed=2000 + i)
+        out, st = gctx.has_match(hs, cse["pattern"])
+        assert gctx.decrypt_radix(gctx.download_radix(out)) == cse["expected"], (i, cse["pattern"], cse["at"])
+        for h in hs + [out]:
+            gctx.release(h)
+
+
 def test_fuzz_encrypted_vs_oracle(gctx):
     """Seeded random patterns (the reference grammar, tests/regex_fuzz.py) on random
     encrypted content of 1-10 chars (engine AUTO), each decrypted result against the
