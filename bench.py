@@ -472,6 +472,8 @@ def main():
         for r, v in enumerate(allr):
             v = v.cpu().tolist()
             d = {"rank": r, "rotations_run": v[len(keys)], "step_ms": v[len(keys) + 1]}
+            if shard == "closure":  # counted once toward value (rank 0) vs run on this rank (its closure)
+                d["rotations_counted"], d["rotations_run"] = v[len(keys)], float(closure_rot[r])
             d.update({kk: round(x, 4) for kk, x in zip(keys, v) if kk in phase or x})
             per_rank.append(d)
     else:
