@@ -158,7 +158,7 @@ class Device {
     int8_t* d_kl_ = nullptr;      // KSK as balanced byte limbs [col*8 + limb][k] (MFMA keyswitch)
     int kl_cols_ = 0;
     bool ks_mfma_ = true;         // FR_KS_MFMA=0: the VALU lincomb+keyswitch kernel
-    size_t ks_mr4_min_ = 128;     // FR_KS_MR4_MIN: batches from this size use 4 row tiles per wave
+    size_t ks_mr4_min_ = 96;      // FR_KS_MR4_MIN: batches from this size use 4 row tiles per wave (k_ks_glds; ab_ks_glds.log: 100 gates 44 -> 37 us, 64 gates no gain)
     int ks_mc_ = 0;               // FR_KS_MC=2: two column tiles per wave in the 4-row-tile shape (else one)
     int ks_split_ = 0;            // FR_KS_SPLIT: K slices (a divisor of kN*ks_level/256; 0: auto)
     int ks_xcd_ = 1;              // FR_KS_XCD=0: plain workgroup order of the MFMA keyswitch (k_ks_mfma)

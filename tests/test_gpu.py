@@ -81,11 +81,12 @@ def test_keyswitch_bit_exact(gctx, oracle_k1):
     assert (got == exp).all()
 
 
-@pytest.mark.parametrize("count", [1, 130, 300, 600])
+@pytest.mark.parametrize("count", [1, 100, 130, 300, 600])
 def test_keyswitch_batch_sizes_bit_exact(gctx, oracle_k1, count):
     """MFMA keyswitch paths (fragment-ordered operands): one row tile per wave with
-    8 K slices (1), 4-row-tile blocking with padding and 5 K slices (130 -> 256
-    rows, 300, 600 -> 640 rows); random (non-message) masks."""
+    8 K slices (1); the LDS-DMA four-row-tile kernel with padding rows: 5 K slices
+    (100 -> 128 rows, 130 -> 256 rows), 2 (300 -> 384 rows) and 1 (600 -> 640 rows);
+    random (non-message) masks."""
     rng = np.random.default_rng(count)
     blocks = rng.integers(0, 2**64 - 1, (count, gctx.lwe_len), dtype=np.uint64, endpoint=True)
     got = gctx.dev_keyswitch(blocks)
