@@ -1,0 +1,88 @@
+/* A plain C99 consumer of include/fheregex.h, built and run by
+ * tests/test_host.py::test_c_abi_consumer (gcc, no GPU): the boundary is usable
+ * from C exactly as declared (the Rust extern block of INTEGRATION.md binds the
+ * same symbols).  Host-only context (device -1): reference parse / Err / panic
+ * behaviour (parser.rs:146-351, engine.rs:189-190), the reference counters of
+ * has_match on a golden vector (engine.rs:256-280), the client key loaded from the
+ * fixture, and GPU entry points refusing loudly with FR_ERR_NO_DEVICE.
+ * Usage: c_abi_consumer <path to tests/golden/client_key>; exit status 0 = pass. */
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "fheregex.h"
+
+static int failures = 0;
+#define CHECK(cond, ...)                           \
+    do {                                           \
+        if (!(cond)) {                             \
+            fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);          \
+            fprintf(stderr, "\n");                 \
+            ++failures;                            \
+        }                                          \
+    } while (0)
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        fprintf(stderr, "usage: %s client_key\n", argv[0]);
+        return 2;
+    }
+    fr_params p;
+    CHECK(fr_default_params(&p) == FR_OK, "default params");
+    CHECK(p.k == 1 && p.N == 2048 && p.n == 742 && p.ks_base_log == 3 && p.ks_level == 5 && p.pbs_base_log == 23 &&
+              p.pbs_level == 1,
+          "PARAM_MESSAGE_2_CARRY_2: k=%d N=%d n=%d", p.k, p.N, p.n);
+
+    /* parser: canonical AST, the reference's Err and panic */
+    char ast[512];
+    CHECK(fr_parse("/abc/", ast, sizeof ast) == FR_OK && strlen(ast) > 0, "parse /abc/");
+    CHECK(fr_parse("/[a-z0-9]+/", ast, sizeof ast) == FR_ERR_PARSE, "[a-z0-9] is Err in the reference grammar");
+    CHECK(strlen(fr_last_error()) > 0, "error message set");
+
+    /* symbolic has_match with the reference's counters: /abc/ on "qqabcq" */
+    fr_plain_result r;
+    memset(&r, 0, sizeof r);
+    CHECK(fr_plain_match("qqabcq", 6, "/abc/", 0, 6, FR_LOWER_FAITHFUL, &r) == FR_OK, "plain match");
+    CHECK(r.result_recorded == 1 && r.result_lowered == 1, "/abc/ in qqabcq: %d %d", r.result_recorded,
+          r.result_lowered);
+    /* golden vectors with the reference's counters (tests/golden/engine_vectors.json) */
+    memset(&r, 0, sizeof r);
+    CHECK(fr_plain_match("ab", 2, "/ab/", 0, 2, FR_LOWER_FAITHFUL, &r) == FR_OK, "plain match ab");
+    CHECK(r.result_recorded == 1 && r.ct_ops == 3 && r.cache_hits == 0, "/ab/ on ab: %d ops %llu hits %llu",
+          r.result_recorded, (unsigned long long)r.ct_ops, (unsigned long long)r.cache_hits);
+    memset(&r, 0, sizeof r);
+    CHECK(fr_plain_match("ab", 2, "/a?b/", 0, 2, FR_LOWER_FAITHFUL, &r) == FR_OK, "plain match a?b");
+    CHECK(r.result_recorded == 1 && r.ct_ops == 6 && r.cache_hits == 1, "/a?b/ on ab: %d ops %llu hits %llu",
+          r.result_recorded, (unsigned long long)r.ct_ops, (unsigned long long)r.cache_hits);
+    memset(&r, 0, sizeof r);
+    CHECK(fr_plain_match("qqabxq", 6, "/abc/", 0, 6, FR_LOWER_THRESHOLD, &r) == FR_OK, "plain match (absent)");
+    CHECK(r.result_recorded == 0 && r.result_lowered == 0, "/abc/ not in qqabxq");
+
+    /* a host-only context: keys load, GPU entry points refuse */
+    fr_ctx* ctx = NULL;
+    CHECK(fr_ctx_create(&p, -1, &ctx) == FR_OK && ctx, "host-only context");
+    FILE* f = fopen(argv[1], "rb");
+    CHECK(f != NULL, "open %s", argv[1]);
+    if (f && ctx) {
+        fseek(f, 0, SEEK_END);
+        const long len = ftell(f);
+        fseek(f, 0, SEEK_SET);
+        unsigned char* blob = (unsigned char*)malloc((size_t)len);
+        CHECK(blob && fread(blob, 1, (size_t)len, f) == (size_t)len, "read client key");
+        CHECK(fr_load_client_key(ctx, blob, (size_t)len) == FR_OK, "load client key: %s", fr_last_error());
+        free(blob);
+        fr_ct content[1] = {0};
+        fr_ct out = 0;
+        CHECK(fr_has_match(ctx, content, 1, "/a/", &out, NULL) == FR_ERR_NO_DEVICE, "has_match needs a device");
+    }
+    if (f) fclose(f);
+    if (ctx) CHECK(fr_ctx_destroy(ctx) == FR_OK, "destroy");
+
+    if (failures) {
+        fprintf(stderr, "%d failure(s)\n", failures);
+        return 1;
+    }
+    printf("c_abi_consumer: ok\n");
+    return 0;
+}

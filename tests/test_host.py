@@ -281,3 +281,23 @@ def test_fuzz_boundary_lowering_vs_oracle():
     for c in cases[::3]:
         pm = F.plain_match(c["content"].encode(), c["pattern"], engine=F.ENGINE_AUTO)
         assert pm.result_lowered == pm.result_recorded == c["expected"], (c["pattern"], c["at"])
+
+
+def test_c_abi_consumer(tmp_path):
+    """include/fheregex.h from plain C99 (gcc -Werror) against the in-tree library: a
+    host-only context, the reference's parse Err, golden counters, the fixture key,
+    FR_ERR_NO_DEVICE on GPU entry points (tests/c_abi_consumer.c)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib_dir = os.path.join(repo, "fhe-regex_amd")
+    exe = str(tmp_path / "c_abi_consumer")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(repo, "include"),
+                    os.path.join(here, "c_abi_consumer.c"), "-o", exe, "-L", lib_dir, "-lfheregex",
+                    "-Wl,-rpath," + lib_dir, "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
+    res = subprocess.run([exe, os.path.join(GOLDEN, "client_key")], capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert "ok" in res.stdout
