@@ -5,7 +5,11 @@
  * behaviour (parser.rs:146-351, engine.rs:189-190), the reference counters of
  * has_match on a golden vector (engine.rs:256-280), the client key loaded from the
  * fixture, and GPU entry points refusing loudly with FR_ERR_NO_DEVICE.
- * Usage: c_abi_consumer <path to tests/golden/client_key>; exit status 0 = pass. */
+ * With a second argument "gpu" (tests/test_gpu.py::test_c_abi_consumer_gpu) it also
+ * runs the engine end to end on device 0 from C: server key, device encryption of the
+ * content (encrypt_str, ciphertext.rs:32-40), has_match (engine.rs:8-42), the
+ * result downloaded and decrypted under the fixture key -- planted and absent.
+ * Usage: c_abi_consumer <path to tests/golden/client_key> [gpu]; exit status 0 = pass. */
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -78,6 +82,53 @@ int main(int argc, char** argv) {
     }
     if (f) fclose(f);
     if (ctx) CHECK(fr_ctx_destroy(ctx) == FR_OK, "destroy");
+
+    if (argc > 2 && strcmp(argv[2], "gpu") == 0) {
+        /* the engine end to end on device 0 */
+        fr_ctx* g = NULL;
+        CHECK(fr_ctx_create(&p, 0, &g) == FR_OK && g, "device context: %s", fr_last_error());
+        f = fopen(argv[1], "rb");
+        if (g && f) {
+            fseek(f, 0, SEEK_END);
+            const long len = ftell(f);
+            fseek(f, 0, SEEK_SET);
+            unsigned char* blob = (unsigned char*)malloc((size_t)len);
+            CHECK(blob && fread(blob, 1, (size_t)len, f) == (size_t)len, "read client key");
+            CHECK(fr_load_client_key(g, blob, (size_t)len) == FR_OK, "load client key: %s", fr_last_error());
+            free(blob);
+            CHECK(fr_gen_server_key(g, 42) == FR_OK, "server key: %s", fr_last_error());
+            const char* texts[2] = {"the quick abc fox", "the quick abx fox"};
+            const uint64_t expect[2] = {1, 0};
+            const size_t lwe = (size_t)p.k * (size_t)p.N + 1;
+            uint64_t* blocks = (uint64_t*)malloc(4 * lwe * sizeof(uint64_t));
+            for (int t = 0; t < 2; ++t) {
+                const size_t n = strlen(texts[t]);
+                fr_ct chars[32];
+                CHECK(fr_encrypt_upload_str(g, texts[t], n, 7 + (uint64_t)t, chars) == FR_OK, "encrypt: %s",
+                      fr_last_error());
+                fr_ct res = 0;
+                fr_match_stats st;
+                memset(&st, 0, sizeof st);
+                CHECK(fr_has_match(g, chars, n, "/abc/", &res, &st) == FR_OK, "has_match: %s", fr_last_error());
+                CHECK(fr_download_radix(g, res, blocks) == FR_OK, "download: %s", fr_last_error());
+                uint64_t v = 99;
+                CHECK(fr_decrypt_radix(g, blocks, &v) == FR_OK && v == expect[t], "/abc/ on '%s': %llu",
+                      texts[t], (unsigned long long)v);
+                CHECK(st.blind_rotations > 0 && st.levels > 0, "stats filled");
+                fr_release(g, res);
+                for (size_t q = 0; q < n; ++q) fr_release(g, chars[q]);
+            }
+            fr_ct one[1];
+            CHECK(fr_encrypt_upload_str(g, "a", 1, 9, one) == FR_OK, "encrypt one char");
+            fr_ct bad = 0;
+            CHECK(fr_has_match(g, one, 1, "/[a-z0-9]+/", &bad, NULL) == FR_ERR_PARSE,
+                  "the reference's Err on the device path");
+            fr_release(g, one[0]);
+            free(blocks);
+        }
+        if (f) fclose(f);
+        if (g) CHECK(fr_ctx_destroy(g) == FR_OK, "destroy device context");
+    }
 
     if (failures) {
         fprintf(stderr, "%d failure(s)\n", failures);

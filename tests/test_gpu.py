@@ -710,6 +710,28 @@ def test_fuzz_scale_vs_oracle(gctx):
             gctx.release(h)
 
 
+@pytest.mark.gpu
+def test_c_abi_consumer_gpu(tmp_path):
+    """The engine end to end from plain C on device 0 (tests/c_abi_consumer.c ... gpu):
+    server key, device encryption, has_match planted and absent, download and decrypt
+    under the fixture key, the reference's Err on the device path."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    here = os.path.dirname(os.path.abspath(__file__))
+    repo = os.path.dirname(here)
+    lib_dir = os.path.join(repo, "fhe-regex_amd")
+    exe = str(tmp_path / "c_abi_consumer")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(repo, "include"),
+                    os.path.join(here, "c_abi_consumer.c"), "-o", exe, "-L", lib_dir, "-lfheregex",
+                    "-Wl,-rpath," + lib_dir, "-Wl,-rpath-link,/opt/rocm/lib"], check=True)
+    res = subprocess.run([exe, os.path.join(here, "golden", "client_key"), "gpu"], capture_output=True, text=True,
+                         timeout=120)
+    assert res.returncode == 0, res.stderr
+    assert "ok" in res.stdout
+
+
 def test_fuzz_boundary_vs_oracle(gctx):
     """30 seeded random patterns on 256-512 encrypted chars with a matching string, or a
     one-character near miss of it, planted at the first or the last start offsets
