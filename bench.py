@@ -15,13 +15,20 @@ k2n1024, BASELINE's "N=1024"); config3 = /^[a-z0-9]+$/ on 256 chars (grammar
 extension: the reference returns Err); config4 = /the/i on 1024 chars;
 config5 = /^a{2,8}(bc|de)+[^xyz]$/ on 512 chars (state-merging engine).
 
-N > 1 (one process per GPU, torch.distributed over RCCL):
-  --scaling weak (default): per-GPU work fixed.  --shard matches (default): every
-    rank runs --matches independent matches of the workload on its own content
-    (no data-path collective; the timing all-reduce only).  --shard starts: --chars
-    start offsets per GPU (content grows with N); each rank matches its start range
-    on the content window those starts read, the per-rank booleans are
-    all-gathered device to device and OR-ed on rank 0 (the reference's ct_or fold).
+N > 1 (one process per GPU, torch.distributed over RCCL).  `--gpus N` with no
+WORLD_SIZE in the environment starts the N rank processes itself (a child
+`python -m torch.distributed.run`, before anything touches the GPU) and exits with
+their status; under an external launcher WORLD_SIZE must equal --gpus.
+  --scaling weak (default): per-GPU work fixed.  --shard starts (default; BASELINE
+    north_star's per-start-offset variants with a final bitor over RCCL): the content
+    is --chars per GPU (the workload's length by default, so N x 256 chars for the
+    metric), rank r owns start offsets [r chars, (r+1) chars) and holds only the
+    content window those starts read; each rank matches its start range
+    (fr_has_match_range), the per-rank booleans are all-gathered device to device and
+    OR-ed on rank 0 (fr_or_many: the reference's ct_or fold, engine.rs:22-35).  The
+    same run also times weak scaling by matches (every rank its own full-length
+    match, no data-path collective) into `weak_matches`, never `value`.
+    --shard matches makes that the timed mode.
   --scaling strong: the named content length is fixed and ONE match is split
     across the ranks (fr_shard_* C-ABI).  --shard closure (default,
     fheregex.run_closure_sharded): the jobs feeding the top of the circuit are
@@ -47,6 +54,8 @@ import argparse
 import hashlib
 import json
 import os
+import re
+import subprocess
 import sys
 import time
 
@@ -139,14 +148,6 @@ def make_content(kind: str, L: int, seed: int = 0) -> bytes:
     raise ValueError(kind)
 
 
-def content_window(L: int, pattern: str, lo: int, hi: int, grammar: int, engine: int, lowering: int):
-    """[wlo, whi): the content positions the circuit of starts [lo, hi) reads
-    (from the lowered schedule, so no --halo guess)."""
-    S = F.schedule_match(L, pattern, lo, hi, lowering=lowering, engine=engine, grammar=grammar)
-    pos = [(-1 - j.in_ref[q]) // 4 for j in S.jobs for q in range(j.n_in) if j.in_ref[q] < 0]
-    return (min(pos), max(pos) + 1) if pos else (lo, lo)
-
-
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -159,11 +160,14 @@ def cpu_model() -> str:
 
 
 def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int, lowering: int,
-                 sample: int, match_max_jobs: int):
+                 sample: int, match_max_jobs: int, content_lwes=None, gpu_words=None):
     """The oracle (oracle/: the CPU restatement of this path, test infrastructure)
     timed on this host: 1-thread and all-threads gate-bootstrap rates
     on a sample of eq-nibble gates, and the CPU end-to-end match of the workload on
-    the same lowered schedule (the reference's serial fold, engine.rs:22-35)."""
+    the same lowered schedule (the reference's serial fold, engine.rs:22-35).  With
+    the GPU's content LWEs and result words, the CPU match runs on those very LWEs
+    and `cpu_gpu_bit_identical` says whether its result equals the GPU's word for
+    word."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle_ffi as of
 
@@ -185,13 +189,17 @@ def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int
     rate_all = sample / tall
     S = F.schedule_match(len(content), pattern, lowering=lowering, engine=engine, grammar=grammar)
     match = {"jobs": len(S.jobs), "levels": len(S.level_off) - 1}
+    identical = None
     if len(S.jobs) <= match_max_jobs:
-        ct = O.encrypt_str(content, seed=7)
+        ct = content_lwes if content_lwes is not None else O.encrypt_str(content, seed=7)
         t0 = time.perf_counter()
         res = O.run_schedule(S, ct)
         match["ms"] = (time.perf_counter() - t0) * 1e3
         match["result_decrypted"] = int(O.decode16(res)[0])
         match["how"] = "measured: every job of the lowered schedule on the CPU, level by level"
+        if gpu_words is not None and content_lwes is not None:
+            identical = bool(np.array_equal(np.asarray(gpu_words, dtype=np.uint64), res))
+            match["inputs"] = "the GPU run's content LWEs (same server-key seed)"
     else:
         match["ms"] = len(S.jobs) / rate_all * 1e3
         match["how"] = f"estimated: jobs / all-threads rate (more than {match_max_jobs} jobs)"
@@ -211,6 +219,7 @@ def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int
         "model": cpu_model(),
         "match_ms": match["ms"],
         "match": match,
+        "cpu_gpu_bit_identical": identical,
         "sample": f"{sample} eq-nibble gate bootstraps (lincomb+KS+BR+SE, k={params.k} N={params.N}, {ring} ring) "
                   f"on {threads} OpenMP threads in {tall:.1f} s; {n1} on 1 thread in {t1:.1f} s",
     }
@@ -228,13 +237,74 @@ def pmc_figures(params, path: str):
         return None
     src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16] if os.path.exists(src) else None
+    shapes = {}
+    for ln in d.get("launches", []):
+        m = re.search(r"<\s*\d+,\s*\d+,\s*\d+,\s*(true|false),\s*(\d+)\s*>", ln.get("kernel", ""))
+        if not m or not ln.get("calls"):
+            continue
+        shape = "throughput" if m.group(1) == "false" else ("pair" if m.group(2) == "2" else "latency")
+        b, c = shapes.get(shape, (0.0, 0))
+        shapes[shape] = (b + ln["hbm_bytes"] * ln["calls"], c + ln["calls"])
     return {"traffic": d.get("hbm_bytes_per_launch"), "valu_per_cu_clk": d.get("valu_per_cu_clk"),
+            "traffic_per_shape": {k: b / c for k, (b, c) in shapes.items()},
             "source": os.path.relpath(path, REPO), "stale": d.get("kernel_sha") != sha}
+
+
+def spawn_ranks(n: int, argv) -> int:
+    """`--gpus N` without a launcher: start N rank processes of this script with
+    torch.distributed.run on 127.0.0.1 (one per GPU) and return their exit status.
+    The caller has touched no GPU (no HIP call, no torch.cuda query) and never
+    re-execs: the ranks are children."""
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def spawn_probe(world: int, rank: int):
+    """--spawn-probe: the rank processes meet over gloo and report, without a GPU
+    (the CPU test of the launcher path)."""
+    import torch
+    import torch.distributed as dist
+
+    if world > 1:
+        dist.init_process_group("gloo")
+        mine = torch.tensor([rank, os.getpid(), os.getppid()], dtype=torch.int64)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        rows = [v.tolist() for v in allr]
+        dist.destroy_process_group()
+    else:
+        rows = [[0, os.getpid(), os.getppid()]]
+    if rank == 0:
+        print(json.dumps({"spawn_probe": True, "n_gpus": world, "ranks": [r[0] for r in rows],
+                          "pids": [r[1] for r in rows], "parent_pids": [r[2] for r in rows]}))
+
+
+def resolve_mode(scaling: str, shard: str, world: int, matches: int):
+    """(strong, shard) of a run: one GPU runs the plain (or batched) match; N > 1 weak
+    defaults to start-offset shards, strong to closure sharding."""
+    strong = scaling == "strong" and world > 1
+    shard = shard or ("closure" if strong else "starts")
+    if world == 1:
+        return False, "matches"
+    if strong != (shard in ("closure", "level")):
+        raise ValueError(f"--shard {shard} does not belong to --scaling {scaling}")
+    if shard != "matches" and matches != 1:
+        raise ValueError("--matches > 1 runs with --shard matches (or N = 1)")
+    return strong, shard
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); N > 1 without WORLD_SIZE set starts the N rank processes itself")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="metric", choices=sorted(WORKLOADS))
@@ -242,10 +312,17 @@ def main():
                     help="N>1: weak = per-GPU work fixed (default); strong = the workload's content split across "
                          "ranks (one match)")
     ap.add_argument("--shard", default="", choices=["", "matches", "starts", "closure", "level"],
-                    help="weak: matches (default; independent matches per rank, no data-path collective) or starts "
-                         "(start-offset shards + RCCL gather + OR); strong: closure (default; each rank runs the "
-                         "dependency closure of its part of the top's inputs, one gather to rank 0) or level (job "
-                         "slices per level, all-gathered level by level)")
+                    help="weak: starts (default; start-offset shards + RCCL all_gather + OR on rank 0) or matches "
+                         "(independent matches per rank, no data-path collective); strong: closure (default; each "
+                         "rank runs the dependency closure of its part of the top's inputs, one gather to rank 0) or "
+                         "level (job slices per level, all-gathered level by level)")
+    ap.add_argument("--spawn-probe", action="store_true",
+                    help="launcher test: the ranks meet over gloo and rank 0 prints who ran (no GPU)")
+    ap.add_argument("--weak-matches-steps", type=int, default=-1,
+                    help="--shard starts: steps of the secondary weak-by-matches timing (-1: --steps; 0: skip)")
+    ap.add_argument("--faithful-steps", type=int, default=1,
+                    help="N=1 metric: timed matches of the reference-structured lowering (FR_LOWER_FAITHFUL) "
+                         "for the `faithful` sub-record (0: skip)")
     ap.add_argument("--matches", type=int, default=1, help="matches per rank per step (fr_has_match_batch)")
     ap.add_argument("--chars", type=int, default=0, help="content chars (strong: total; weak: per GPU); 0: workload's")
     ap.add_argument("--pattern", default="", help="override the workload's pattern")
@@ -268,6 +345,16 @@ def main():
                     help="PMC summary of the BR kernel (tools/pmc_summary.py); default: profiles/r03/"
                          "pmc_summary.json at k1n2048, pmc_summary_k2n1024.json at k2n1024")
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error("--gpus must be >= 1")
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+    if env_world is not None and int(env_world) != args.gpus:
+        ap.error(f"--gpus {args.gpus} disagrees with WORLD_SIZE={env_world} from the launcher")
+    if args.spawn_probe:
+        spawn_probe(int(env_world or 1), int(os.environ.get("RANK", "0")))
+        return
     if not args.pmc:
         args.pmc = os.path.join(REPO, "profiles", "r03",
                                 "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json")
@@ -284,14 +371,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    strong = args.scaling == "strong" and world > 1
-    shard = args.shard or ("closure" if strong else "matches")
-    if world == 1:
-        shard = "matches"  # one GPU: the plain (or batched) match
-    elif strong != (shard in ("closure", "level")):
-        ap.error(f"--shard {shard} does not belong to --scaling {args.scaling}")
-    if world > 1 and shard != "matches" and args.matches != 1:
-        ap.error("--matches > 1 runs with --shard matches (or N = 1)")
+    try:
+        strong, shard = resolve_mode(args.scaling, args.shard, world, args.matches)
+    except ValueError as e:
+        ap.error(str(e))
     import torch
 
     dist = None
@@ -339,20 +422,24 @@ def main():
     # content each rank holds: the window its starts read (start shards), else all of it
     if starts:
         lo, hi = F.shard_starts(L, world, rank)
-        wlo, whi = content_window(L, pattern, lo, hi, grammar, engine, lowering)
+        wlo, whi = F.content_window(L, pattern, lo, hi, lowering=lowering, engine=engine, grammar=grammar)
     else:
         lo, hi, wlo, whi = 0, L, 0, L
 
-    def encrypt(c, seed):
+    lwes0 = []  # the first content's LWEs (the CPU baseline evaluates the same words)
+
+    def encrypt(c, seed, keep=False):
         hs = [F.NULL_CT] * L
         if whi > wlo:
             msgs = [(ch >> (2 * b)) & 3 for ch in c[wlo:whi] for b in range(4)]
             blocks = ctx.encrypt_blocks(msgs, seed=seed, first_block=4 * wlo).reshape(whi - wlo, 4, ctx.lwe_len)
+            if keep:
+                lwes0.append(blocks)
             for i, h in enumerate(ctx.upload_radix(blocks)):
                 hs[wlo + i] = h
         return hs
 
-    batch = [encrypt(c, 7 + 1000 * rank + m) for m, c in enumerate(contents)]
+    batch = [encrypt(c, 7 + 1000 * rank + m, keep=m == 0) for m, c in enumerate(contents)]
     handles = batch[0]
     handles_np = np.asarray(handles, dtype=np.uint32)  # passed without a per-call ctypes copy
 
@@ -453,6 +540,7 @@ def main():
     elapsed = time.perf_counter() - t0
     t_after = ctx.device_timers()
     ctx.set_profiling(False)
+    ms_per_step_local = elapsed / args.steps * 1e3
 
     per_rank = None
     if dist is not None:
@@ -480,8 +568,11 @@ def main():
         total_rot = float(rot_local)
 
     result = None
+    words0 = None
     if rank == 0:
-        result = [ctx.decrypt_radix(ctx.download_radix(o)) for o in outs]
+        words = [ctx.download_radix(o) for o in outs]
+        words0 = words[0][0] if words else None
+        result = [ctx.decrypt_radix(w) for w in words]
         exp = expected if shard == "matches" else expected[:1]
         if result != exp:
             print(f"WARNING: decrypted results {result} != expected {exp}", file=sys.stderr)
@@ -507,6 +598,65 @@ def main():
         for (o, _), hs in zip(res, hss):
             for h in list(hs) + [o]:
                 ctx.release(int(h))
+
+    weak_matches = None
+    wm_steps = args.steps if args.weak_matches_steps < 0 else args.weak_matches_steps
+    if shard == "starts" and world > 1 and wm_steps > 0:
+        # secondary record: weak scaling by matches (every rank one full-length match of
+        # the workload on its own content per step, no data-path collective)
+        own = make_content(kind, chars, seed=rank)
+        own_hs = np.asarray(ctx.encrypt_upload_str(own, seed=9000 + rank), dtype=np.uint32)
+        o, _ = ctx.has_match(own_hs, pattern)  # warm-up (plan)
+        ctx.release(o)
+        barrier()
+        t = time.perf_counter()
+        wrot = 0
+        for i in range(wm_steps):
+            o, stw = ctx.has_match(own_hs, pattern)
+            wrot += stw.blind_rotations
+            if i + 1 < wm_steps:
+                ctx.release(o)
+        barrier()
+        wel = time.perf_counter() - t
+        ok = ctx.decrypt_radix(ctx.download_radix(o)) == F.plain_match(
+            own, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+        ctx.release(o)
+        tt = torch.tensor([wel, float(wrot), float(ok)], dtype=torch.float64, device=coll_dev)
+        mx, sm = tt[:1].clone(), tt[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        weak_matches = {"value": float(sm[0]) / float(mx[0]), "unit": "gate-bootstraps/s",
+                        "ms_per_step": float(mx[0]) * 1e3 / wm_steps, "steps": wm_steps,
+                        "workload": f"{pattern} on {chars} chars, one match per rank per step on its own content",
+                        "results_ok_ranks": int(sm[1]), "note": "secondary: weak scaling by matches, never `value`"}
+        for h in own_hs:
+            ctx.release(int(h))
+
+    faithful = None
+    if args.faithful_steps > 0 and world == 1 and M == 1 and rank == 0 and lowering == F.LOWER_THRESHOLD:
+        # the reference-structured lowering (one gate group per smart_* op, execution.rs:64-195)
+        # on the same content: its PBS count and levels are the reference's op structure
+        ctx.set_lowering(F.LOWER_FAITHFUL)
+        t = time.perf_counter()
+        o, stf = ctx.has_match(handles_np, pattern)
+        torch.cuda.synchronize()
+        cold_ms = (time.perf_counter() - t) * 1e3
+        ctx.release(o)
+        t = time.perf_counter()
+        for i in range(args.faithful_steps):
+            o, stf = ctx.has_match(handles_np, pattern)
+            if i + 1 < args.faithful_steps:
+                ctx.release(o)
+        torch.cuda.synchronize()
+        fms = (time.perf_counter() - t) * 1e3 / args.faithful_steps
+        fres = ctx.decrypt_radix(ctx.download_radix(o))
+        ctx.release(o)
+        ctx.set_lowering(lowering)
+        faithful = {"lowering": "faithful (FR_LOWER_FAITHFUL: eq/gt/le = 3 PBS, and/or = 1, not linear)",
+                    "match_ms": fms, "first_call_ms": cold_ms, "steps": args.faithful_steps,
+                    "pbs": int(stf.pbs), "blind_rotations": int(stf.blind_rotations), "levels": int(stf.levels),
+                    "pbs_per_s": stf.pbs / (fms / 1e3), "result_decrypted": fres,
+                    "vs_threshold_ms": ms_per_step_local}
 
     kernel = None
     if args.saturate and rank == 0:
@@ -545,16 +695,24 @@ def main():
                                                      "pair_br_ms", "pair_launches", "pair_gates")}
     cus = 256
 
-    def shape_line(ms, launches, gates, per_wg=1):
+    def shape_line(name, ms, launches, gates, per_wg=1):
         """one launch shape: algorithmic TFLOP/s, also per active CU (min(workgroups, 256) CUs; per_wg
-        bootstraps per workgroup)"""
+        bootstraps per workgroup); the contract's HBM figures at this shape: algorithmic GGSW bytes
+        (bpp per bootstrap) and the PMC's physical bytes per launch of the shape, over its launch time"""
         if ms <= 0 or launches == 0:
             return None
         tf = gates * fpp / (ms / 1e3) / 1e12
         active = min(gates / launches / per_wg, cus)
+        avg_s = ms / launches / 1e3
+        alg = gates / launches * bpp / avg_s / 1e9
+        phys_b = (pmc or {}).get("traffic_per_shape", {}).get(name)
+        phys = phys_b / avg_s / 1e9 if phys_b else None
         return {"launches": int(launches), "bootstraps_per_launch": gates / launches, "avg_ms": ms / launches,
                 "achieved_tflops": tf, "frac": tf / FP64_VECTOR_PEAK_TFLOPS,
-                "frac_of_active_cus": tf / (FP64_VECTOR_PEAK_TFLOPS * active / cus)}
+                "frac_of_active_cus": tf / (FP64_VECTOR_PEAK_TFLOPS * active / cus),
+                "hbm_algorithmic_GBps": alg, "hbm_algorithmic_frac": alg / HBM_PEAK_GBS,
+                "hbm_physical_bytes_per_launch": phys_b, "hbm_physical_GBps": phys,
+                "hbm_physical_frac": phys / HBM_PEAK_GBS if phys is not None else None}
 
     achieved_tf = br_gates * fpp / (br_ms / 1e3) / 1e12 if br_ms > 0 else 0.0
     alg_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
@@ -564,7 +722,7 @@ def main():
     cpu = None
     if args.cpu_sample > 0 and world == 1:
         cpu = cpu_baseline(params, content, pattern, grammar, engine, lowering, args.cpu_sample,
-                           args.cpu_match_max_jobs)
+                           args.cpu_match_max_jobs, lwes0[0] if lwes0 else None, words0)
     ms_per_step = elapsed / args.steps * 1e3
     ring_name = "fft" if params.ring == F.RING_FFT else "rns"
     coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
@@ -630,9 +788,9 @@ def main():
             "br_avg_ms": br_avg_ms,
             "br_gates_per_launch": br_gates / max(br_launches, 1),
             "per_shape": {
-                "latency": shape_line(lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
-                "pair": shape_line(lat["pair_br_ms"], lat["pair_launches"], lat["pair_gates"], 2),
-                "throughput": shape_line(br_ms - lat["lat_br_ms"] - lat["pair_br_ms"],
+                "latency": shape_line("latency", lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
+                "pair": shape_line("pair", lat["pair_br_ms"], lat["pair_launches"], lat["pair_gates"], 2),
+                "throughput": shape_line("throughput", br_ms - lat["lat_br_ms"] - lat["pair_br_ms"],
                                          br_launches - lat["lat_launches"] - lat["pair_launches"],
                                          br_gates - lat["lat_gates"] - lat["pair_gates"]),
             },
@@ -656,6 +814,8 @@ def main():
             "pmc_source": pmc["source"] if pmc else None,
             "pmc_stale": pmc["stale"] if pmc else None,
         },
+        "weak_matches": weak_matches,
+        "faithful": faithful,
         "kernel_saturated": kernel,
         "latency_probe": probe,
         "cpu_baseline": cpu,

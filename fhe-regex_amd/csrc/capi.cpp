@@ -629,11 +629,16 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
         st->host_ms = t1 - t0;
         st->device_ms = t2 - t1;
         st->plan_cached = cached ? 1 : 0;
-        const DeviceTimers& after = dev.timers();
-        st->br_kernel_ms = after.br_ms - before.br_ms;
-        st->ks_kernel_ms = after.ks_ms - before.ks_ms;
-        st->br_launches = after.br_launches - before.br_launches;
-        st->br_gates = after.br_gates - before.br_gates;
+        if (!ctx->async_match) {
+            // blocking call: this match's timers resolved at its sync.  An asynchronous
+            // call returns before its kernels ran, so its timers are left 0 here (read
+            // them with fr_device_timers after a synchronising call instead)
+            const DeviceTimers& after = dev.timers();
+            st->br_kernel_ms = after.br_ms - before.br_ms;
+            st->ks_kernel_ms = after.ks_ms - before.ks_ms;
+            st->br_launches = after.br_launches - before.br_launches;
+            st->br_gates = after.br_gates - before.br_gates;
+        }
     }
 }
 
@@ -771,8 +776,9 @@ int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* lu
 int fr_set_profiling(fr_ctx* ctx, int32_t on) {
     FR_TRY({
         NEED(ctx);
-        if (on < 0 || on > 2) throw Error(FR_ERR_INVALID, "profiling level: 0, 1 or 2");
-        ctx->device().set_profiling(on);
+        // 0 off, 2 the keyswitch timers too; any other nonzero value is level 1 (the
+        // function took a boolean before the levels existed)
+        ctx->device().set_profiling(on == 2 ? 2 : (on ? 1 : 0));
     })
 }
 

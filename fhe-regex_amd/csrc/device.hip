@@ -1729,6 +1729,7 @@ void Device::sync() {
 // ---------------------------------------------------------------- tests
 void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    HIP_CHECK(hipStreamSynchronize(STREAM));  // queued matches read d_ks_ / d_gates_ (blind_rotate_host)
     std::vector<int> slots(count);
     std::vector<DevGate> gates(count);
     for (size_t i = 0; i < count; ++i) slots[i] = alloc_slot();
@@ -1754,6 +1755,9 @@ void Device::keyswitch_host(const uint64_t* in, size_t count, uint64_t* out) {
 
 void Device::blind_rotate_host(const uint64_t* ks_in, const uint8_t* luts, size_t count, uint64_t* out) {
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    // an asynchronous match may still read d_ks_ / d_gates_ on STREAM; the plain
+    // copies below run on the null stream, which does not wait for a non-blocking one
+    HIP_CHECK(hipStreamSynchronize(STREAM));
     ensure_batch(count);
     const int ks = p_.ks_stride();
     for (size_t i = 0; i < count; ++i)
@@ -1780,6 +1784,7 @@ void Device::blind_rotate_multi_host(const uint64_t* ks_in, const uint8_t* luts,
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
     if (n_out < 1 || n_out > MAX_OUT || direct < 0 || direct > 2 || (direct && n_out != 1))
         throw Error(FR_ERR_INVALID, "bad n_out");
+    HIP_CHECK(hipStreamSynchronize(STREAM));  // as blind_rotate_host: queued matches read these buffers
     ensure_batch(1);
     HIP_CHECK(hipMemcpy(d_ks_, ks_in, 8 * (size_t)(p_.n + 1), hipMemcpyHostToDevice));
     DevGate g;

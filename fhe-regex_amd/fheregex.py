@@ -879,6 +879,17 @@ def schedule_match(n_chars: int, pattern: str, start_lo: int = 0, start_hi: Opti
     return Schedule(list(jobs[:nj.value]), list(off), out3[0], out3[1], out3[2], n_gates)
 
 
+def content_window(n_chars: int, pattern: str, start_lo: int, start_hi: int, lowering: int = LOWER_THRESHOLD,
+                   engine: int = ENGINE_AUTO, grammar: int = GRAMMAR_REFERENCE) -> Tuple[int, int]:
+    """[wlo, whi): the content positions the circuit of starts [start_lo, start_hi)
+    reads, from its lowered schedule (a start's branch reads the characters after
+    it, engine.rs:45-214): a start-offset shard needs only this window of the
+    content.  (lo, lo) when the circuit reads no content."""
+    S = schedule_match(n_chars, pattern, start_lo, start_hi, lowering=lowering, engine=engine, grammar=grammar)
+    pos = [(-1 - j.in_ref[q]) // 4 for j in S.jobs for q in range(j.n_in) if j.in_ref[q] < 0]
+    return (min(pos), max(pos) + 1) if pos else (start_lo, start_lo)
+
+
 def header_symbols() -> List[str]:
     import re
     txt = open(HEADER).read()

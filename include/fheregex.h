@@ -89,6 +89,9 @@ typedef struct {
     uint64_t max_level_width;
     double host_ms;         /* parse + enumerate + record + lower + compile (plan-cache hit: the lookup) */
     double device_ms;       /* device execution, wall (fr_set_async on: until the launches are enqueued) */
+    /* This match's kernel timers (fr_set_profiling on).  Filled only by a blocking call
+     * (fr_set_async(ctx, 0)); an asynchronous call returns before its kernels run and
+     * leaves them 0: read fr_device_timers after a synchronising call instead. */
     double br_kernel_ms;    /* sum of blind-rotation kernel durations (HIP events) */
     double ks_kernel_ms;    /* sum of lincomb+keyswitch kernel durations (HIP events) */
     uint64_t br_launches;
@@ -344,7 +347,8 @@ int fr_set_multi_value(fr_ctx* ctx, int32_t on);
 /* Device profiling: 0 off; 1 blind-rotation timers (HIP events stamped by each blind
  * rotation launch itself, hipExtLaunchKernel: no marker packets, no syncs; what bench.py's
  * timed region uses); 2 also the keyswitch timers (two more stamped launches per level,
- * ~30 us per /abc/ x 256 match).  Timers resolve at the next synchronisation. */
+ * ~30 us per /abc/ x 256 match).  Timers resolve at the next synchronisation.  Any
+ * nonzero value other than 2 is level 1. */
 int fr_set_profiling(fr_ctx* ctx, int32_t on);
 
 /* ----- single-stage device entry points (parity tests of each kernel) ----- */

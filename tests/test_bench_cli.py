@@ -1,0 +1,62 @@
+"""bench.py's launcher path on the CPU: `--gpus N` with no WORLD_SIZE starts the N
+rank processes itself (torch.distributed.run as a child, before any GPU call), an
+external launcher's WORLD_SIZE must agree with --gpus, and the N > 1 default is
+north_star's start-offset shards."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(REPO, "bench.py")
+sys.path.insert(0, REPO)
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR",
+                                                           "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_spawns_ranks(n):
+    res = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--spawn-probe"], capture_output=True, text=True,
+                         timeout=240, env=_env())
+    assert res.returncode == 0, res.stderr[-2000:]
+    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, res.stdout  # one JSON line, from rank 0
+    d = json.loads(lines[0])
+    assert d["spawn_probe"] and d["n_gpus"] == n and d["ranks"] == list(range(n))
+    assert len(set(d["pids"])) == n
+    assert len(set(d["parent_pids"])) == 1  # siblings under one launcher child of bench.py
+
+
+def test_single_gpu_runs_in_process():
+    res = subprocess.run([sys.executable, BENCH, "--spawn-probe"], capture_output=True, text=True, timeout=120,
+                         env=_env())
+    assert res.returncode == 0, res.stderr[-2000:]
+    d = json.loads(res.stdout.strip().splitlines()[-1])
+    assert d["n_gpus"] == 1 and d["ranks"] == [0]
+    assert d["parent_pids"] == [os.getpid()]  # no launcher in between
+
+
+def test_world_size_must_match_gpus():
+    res = subprocess.run([sys.executable, BENCH, "--gpus", "4", "--spawn-probe"], capture_output=True, text=True,
+                         timeout=120, env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"))
+    assert res.returncode == 2 and "disagrees with WORLD_SIZE=2" in res.stderr
+
+
+def test_mode_defaults():
+    import bench
+    assert bench.resolve_mode("weak", "", 1, 1) == (False, "matches")
+    assert bench.resolve_mode("weak", "", 8, 1) == (False, "starts")
+    assert bench.resolve_mode("weak", "matches", 8, 4) == (False, "matches")
+    assert bench.resolve_mode("strong", "", 8, 1) == (True, "closure")
+    assert bench.resolve_mode("strong", "level", 2, 1) == (True, "level")
+    with pytest.raises(ValueError):
+        bench.resolve_mode("weak", "closure", 2, 1)
+    with pytest.raises(ValueError):
+        bench.resolve_mode("weak", "starts", 2, 4)

@@ -658,7 +658,44 @@ def test_profiling_timers(gctx, level):
     assert t1["br_ms"] > t0["br_ms"]
     assert (t1["ks_ms"] > t0["ks_ms"]) == (level == 2)
     assert np.array_equal(gctx.download_radix(out), gctx.download_radix(ref))
-    for h in hs + [ref, out]:
+    # a blocking call fills the match's own timers; an asynchronous one leaves them 0
+    assert st.br_launches == 0 and st.br_kernel_ms == 0.0
+    gctx.set_async(False)
+    gctx.set_profiling(level)
+    try:
+        out2, st2 = gctx.has_match(hs, "/abc/")
+    finally:
+        gctx.set_profiling(False)
+        gctx.set_async(True)
+    assert st2.br_launches == st2.levels and st2.br_gates == st2.blind_rotations and st2.br_kernel_ms > 0
+    assert (st2.ks_kernel_ms > 0) == (level == 2)
+    for h in hs + [ref, out, out2]:
+        gctx.release(h)
+
+
+def test_async_match_then_host_hooks(gctx, oracle_k1):
+    """An asynchronous has_match still queued when the single-stage test hooks write
+    their inputs: both results stay right."""
+    O = oracle_k1
+    hs = gctx.upload_radix(gctx.encrypt_str("qq" * 60 + "abc" + "q" * 61, seed=15))
+    ref, _ = gctx.has_match(hs, "/abc/")
+    ref_w = gctx.download_radix(ref)
+    ks = O.keyswitch(O.encrypt_blocks([5, 9, 2], seed=16))
+    luts = [[(3 * m + j) % 16 for m in range(16)] for j in range(3)]
+    for _ in range(2):
+        out, _ = gctx.has_match(hs, "/abc/")  # queued, not synchronised
+        dev = gctx.dev_blind_rotate(ks, luts)
+        for j in range(3):
+            assert (dev[j] == O.blind_rotate(ks[j], luts[j])).all(), j
+        out2, _ = gctx.has_match(hs, "/abc/")
+        mv = gctx.dev_blind_rotate_multi(ks[0], luts[:2])
+        assert (mv == O.blind_rotate_multi(ks[0], luts[:2])).all()
+        out3, _ = gctx.has_match(hs, "/abc/")
+        assert (gctx.dev_keyswitch(O.encrypt_blocks([7], seed=17)) == O.keyswitch(O.encrypt_blocks([7], seed=17))).all()
+        for o in (out, out2, out3):
+            assert np.array_equal(gctx.download_radix(o), ref_w)
+            gctx.release(o)
+    for h in hs + [ref]:
         gctx.release(h)
 
 
@@ -778,3 +815,108 @@ def test_fuzz_encrypted_vs_oracle(gctx):
         for h in hs + [out]:
             gctx.release(h)
         n += 1
+
+
+# ------------------------------------------------ whole matches, word for word
+def _match_words_vs_oracle(gctx, O, content, pattern, seed, engine=F.ENGINE_AUTO, grammar=F.GRAMMAR_REFERENCE):
+    """One has_match on the device against the oracle's evaluation of the same lowered
+    schedule (fr_schedule_match: fr_job semantics, oracle_ffi.run_schedule) on the same
+    content LWEs and the same server key: the result ciphertext word for word
+    (execution.rs:64-222 and the fold engine.rs:22-35, through every level's keyswitch
+    and blind rotation)."""
+    ct = gctx.encrypt_str(content, seed=seed)
+    hs = gctx.upload_radix(ct)
+    out, st = gctx.has_match(hs, pattern)
+    got = gctx.download_radix(out)
+    S = F.schedule_match(len(content), pattern, engine=engine, grammar=grammar)
+    assert (len(S.jobs), len(S.level_off) - 1) == (st.blind_rotations, st.levels)
+    exp = O.run_schedule(S, ct)
+    assert np.array_equal(got[0], exp), (pattern, len(content))
+    assert not got[1:].any()  # blocks 1..3 of the boolean radix: trivial zeros
+    for h in hs + [out]:
+        gctx.release(h)
+    return int(O.decode16(exp)[0] == 1)
+
+
+def test_match_words_abc_64(gctx, oracle_k1):
+    rng = np.random.default_rng(31)
+    s = _printable(rng, 64).replace("abc", "abd")
+    assert _match_words_vs_oracle(gctx, oracle_k1, s[:40] + "abc" + s[43:], "/abc/", 32) == 1
+    assert _match_words_vs_oracle(gctx, oracle_k1, s, "/abc/", 33) == 0
+
+
+def test_match_words_range_64(gctx, oracle_k1):
+    rng = np.random.default_rng(34)
+    s = "".join(chr(c) for c in rng.integers(ord("b"), ord("z") + 1, 64))
+    assert _match_words_vs_oracle(gctx, oracle_k1, s, "/^[a-z]+$/", 35) == 1
+    assert _match_words_vs_oracle(gctx, oracle_k1, s[:50] + "A" + s[51:], "/^[a-z]+$/", 36) == 0
+
+
+def test_match_words_config5_small(gctx, oracle_k1):
+    pat = "/^a{2,8}(bc|de)+[^xyz]$/"
+    for i, s in enumerate(["aaabcdebcf", "aaabcdebcx", "aadef"]):
+        assert _match_words_vs_oracle(gctx, oracle_k1, s, pat, 37 + i) == ro.has_match_reach(s, pat), s
+
+
+@pytest.mark.parametrize("case", [3, 9, 11, 17, 19])
+def test_match_words_fuzz_scale(gctx, oracle_k1, case):
+    """Five fuzz_scale.json cases of 500-950 rotations (case 9: 204 dependent levels)."""
+    cse = load("fuzz_scale.json")["cases"][case]
+    assert _match_words_vs_oracle(gctx, oracle_k1, cse["content"], cse["pattern"], 3000 + case) == cse["expected"]
+
+
+# ------------------------------------- start-offset shards across contexts
+@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("where", ["boundary", "absent"])
+def test_start_shards_two_contexts_config4(gctx, key_blob, world, where):
+    """north_star's start-offset shards (engine.rs:15-35) with one context per rank on
+    device 0: each context holds only the content window its start range reads
+    (F.content_window), runs fr_has_match_range, exports its boolean device to device
+    into its row of one buffer (fr_export_bool_device); the first context imports the
+    rows (fr_import_bool_device) and ORs them (fr_or_many).  BASELINE config 4
+    (/the/i on 1024 chars) with "ThE" across a shard boundary, and absent."""
+    import torch
+    p = gctx.params
+    L, pat = 1024, "/the/i"
+    rng = np.random.default_rng(47)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
+    s = bytearray(rng.choice(alpha, L))
+    for i in range(L - 2):
+        if bytes(s[i:i + 3]).lower() == b"the":
+            s[i + 2] = ord("x")
+    if where == "boundary":
+        cut = F.shard_starts(L, world, 1)[0]  # first start of rank 1: "ThE" starts on rank 0's last start
+        s[cut - 1:cut + 2] = b"ThE"
+    s = bytes(s)
+    exp = ro.has_match_reach(s.decode(), pat)
+    assert exp == (1 if where == "boundary" else 0)
+    ctxs = [gctx]
+    for _ in range(world - 1):
+        c = F.Context(device=0, params=F.default_params(k=p.k, N=p.N, ring=p.ring))
+        c.load_client_key(key_blob)
+        c.gen_server_key(SEED)
+        ctxs.append(c)
+    buf = torch.zeros((world, gctx.lwe_len), dtype=torch.int64, device="cuda:0")
+    held = []
+    for r, c in enumerate(ctxs):
+        lo, hi = F.shard_starts(L, world, r)
+        wlo, whi = F.content_window(L, pat, lo, hi)
+        assert lo <= wlo and whi <= min(L, hi + 2)  # /the/ reads at most 2 characters past a start
+        hs = [F.NULL_CT] * L
+        win = c.upload_radix(c.encrypt_str(s[wlo:whi], seed=60 + r))
+        hs[wlo:whi] = win
+        out, _ = c.has_match(hs, pat, lo, hi)
+        assert c.decrypt_radix(c.download_radix(out)) == int(any(s[i:i + 3].lower() == b"the" for i in range(lo, hi)))
+        c.export_bool_device([out], buf[r].data_ptr())
+        held.append((c, win + [out]))
+    torch.cuda.synchronize()
+    parts = gctx.import_bool_device(buf.data_ptr(), world)
+    res = gctx.or_many(parts)
+    assert gctx.decrypt_radix(gctx.download_radix(res)) == exp
+    for c, hs in held:
+        for h in hs:
+            c.release(h)
+    for h in parts + [res]:
+        gctx.release(h)
+    for c in ctxs[1:]:
+        c.close()
