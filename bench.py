@@ -264,7 +264,12 @@ def spawn_ranks(n: int, argv) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL)
-    return subprocess.call(cmd, env=env)
+    # the ranks' stdout: the JSON line passes, anything else (launcher / gloo chatter) goes to stderr
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for line in proc.stdout:
+        (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    return proc.wait()
 
 
 def spawn_probe(world: int, rank: int):
@@ -484,34 +489,65 @@ def main():
                     times["top_ms"] = times.get("top_ms", 0.0) + (time.perf_counter() - t) * 1e3
                 return [out], mine + plan.jobs(plan.levels - 1), st
             return [], mine, plan.stats
-        # start-offset shards
-        t = time.perf_counter()
-        out, st = ctx.has_match(handles, pattern, lo, hi)
-        buf = torch.empty(ctx.lwe_len, dtype=torch.int64, device=f"cuda:{device}")
-        ctx.export_bool_device([out], buf.data_ptr())
-        ctx.release(out)
-        if times is not None:
-            times["starts_ms"] = times.get("starts_ms", 0.0) + (time.perf_counter() - t) * 1e3
-        t = time.perf_counter()
-        recv = torch.cat(gather(buf))  # [world * lwe_len] on this GPU
-        torch.cuda.synchronize()
-        if times is not None:
-            times["gather_ms"] = times.get("gather_ms", 0.0) + (time.perf_counter() - t) * 1e3
+        raise AssertionError("start shards run starts_pipeline")
+
+    rccl = args.dist_backend == "nccl"
+    lib_stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=torch.device("cuda", device)) if starts else None
+
+    def starts_pipeline(n, times=None):
+        """n start-sharded matches (north_star's per-start-offset variants + final bitor,
+        engine.rs:15-35): per step every rank enqueues its start range's match, exports its
+        boolean device to device into that step's row (stream-ordered) and all-gathers the
+        row (RCCL on torch's stream, ordered after the export by an event on the library's
+        stream; the host never waits between matches).  Rank 0 then ORs every step's
+        gathered booleans in ONE launch (n independent threshold ORs).  gloo (a rehearsal:
+        ranks sharing one GPU) stages the gather through the host.  Returns ([result per
+        step] on rank 0, rotations this rank ran, last stats)."""
+        send = torch.zeros((n, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        recv = torch.zeros((n, world, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        rot, st = 0, None
+        for i in range(n):
+            t = time.perf_counter()
+            out, st = ctx.has_match(handles_np, pattern, lo, hi)
+            rot += st.blind_rotations
+            if rccl:
+                ctx.export_bool_device_async([out], send[i].data_ptr())
+                ev = torch.cuda.Event()
+                ev.record(lib_stream)
+                torch.cuda.current_stream().wait_event(ev)
+            else:
+                ctx.export_bool_device([out], send[i].data_ptr())
+            ctx.release(out)  # stream-ordered: a later user of its slot runs after the export
+            t2 = time.perf_counter()
+            if rccl:
+                dist.all_gather_into_tensor(recv[i].view(-1), send[i])
+            else:
+                for r, b in enumerate(gather(send[i])):
+                    recv[i, r].copy_(b)
+            if times is not None:
+                times["starts_ms"] = times.get("starts_ms", 0.0) + (t2 - t) * 1e3
+                times["gather_ms"] = times.get("gather_ms", 0.0) + (time.perf_counter() - t2) * 1e3
+        torch.cuda.synchronize()  # the gathers (torch's stream) before the library reads recv
         if rank != 0:
-            return [], st.blind_rotations, st
+            return [], rot, st
         t = time.perf_counter()
-        parts = ctx.import_bool_device(recv.data_ptr(), world)
-        res = ctx.or_many(parts)
+        parts = ctx.import_bool_device(recv.data_ptr(), n * world)
+        if world <= 16:
+            res = ctx.or_each([parts[i * world:(i + 1) * world] for i in range(n)])
+            rot += n
+        else:
+            res = [ctx.or_many(parts[i * world:(i + 1) * world]) for i in range(n)]
+            rot += 2 * n
         for h in parts:
             ctx.release(h)
         if times is not None:
             times["or_ms"] = times.get("or_ms", 0.0) + (time.perf_counter() - t) * 1e3
-        return [res], st.blind_rotations + (1 if world <= 16 else 2), st
+        return res, rot, st
 
     first_call = None
     for _ in range(args.warmup):
         t = time.perf_counter()
-        o, _, st0 = step()
+        o, _, st0 = starts_pipeline(1) if starts else step()
         if first_call is None:  # cold call: parse, record, lower, compile, plan upload, and its device time
             torch.cuda.synchronize()
             first_call = {"host_ms": st0.host_ms, "wall_ms": (time.perf_counter() - t) * 1e3,
@@ -527,7 +563,10 @@ def main():
     host_ms = 0.0
     outs = []
     st = None
-    for i in range(args.steps):
+    if starts:
+        step_outs, rot_local, st = starts_pipeline(args.steps, phase)
+        outs = step_outs[-1:]
+    for i in range(0 if starts else args.steps):
         o, rot, st = step(phase)
         rot_local += rot
         host_ms += st.host_ms if shard == "matches" else 0.0
@@ -569,10 +608,16 @@ def main():
 
     result = None
     words0 = None
+    starts_ok = None
     if rank == 0:
         words = [ctx.download_radix(o) for o in outs]
         words0 = words[0][0] if words else None
         result = [ctx.decrypt_radix(w) for w in words]
+        if starts:  # every step's OR, not just the last
+            starts_ok = all(ctx.decrypt_radix(ctx.download_radix(o)) == expected[0] for o in step_outs)
+            for o in step_outs:
+                ctx.release(o)
+            outs = []
         exp = expected if shard == "matches" else expected[:1]
         if result != exp:
             print(f"WARNING: decrypted results {result} != expected {exp}", file=sys.stderr)
@@ -631,6 +676,23 @@ def main():
                         "results_ok_ranks": int(sm[1]), "note": "secondary: weak scaling by matches, never `value`"}
         for h in own_hs:
             ctx.release(int(h))
+
+    step_latency = None
+    if starts:
+        # latency of one start-sharded match end to end (match, export, gather, the OR on
+        # rank 0), synchronised before and after; the timed region pipelines these
+        lat_ms = []
+        for _ in range(3):
+            barrier()
+            t = time.perf_counter()
+            o, _, _ = starts_pipeline(1)
+            barrier()
+            lat_ms.append((time.perf_counter() - t) * 1e3)
+            for h in o:
+                ctx.release(h)
+        step_latency = {"ms_min": min(lat_ms), "ms_mean": sum(lat_ms) / len(lat_ms), "runs": len(lat_ms),
+                        "what": "one start-sharded match end to end (rank 0's view after barriers): the ranks' "
+                                "matches, the boolean all-gather and the OR on rank 0"}
 
     faithful = None
     if args.faithful_steps > 0 and world == 1 and M == 1 and rank == 0 and lowering == F.LOWER_THRESHOLD:
@@ -737,7 +799,9 @@ def main():
     elif shard == "level":
         par = f"level-sharded x{world} (job slices per level, {coll} all_gather of each level's LWEs)"
     else:
-        par = f"start-offset shards x{world} ({coll} all_gather of the per-rank booleans, OR on rank 0)"
+        par = (f"start-offset shards x{world} (each rank its start range on its content window; {coll} "
+               f"all_gather of the per-rank booleans, stream-ordered after each match; rank 0 ORs every step's "
+               f"booleans in one launch at the end of the timed region)")
     work = f"{args.workload}: {pattern} on {L} chars" + (f" ({chars} per GPU)" if starts else "")
     if M > 1 or (world > 1 and shard == "matches"):
         work += f", {M} match(es) per GPU per step"
@@ -814,6 +878,8 @@ def main():
             "pmc_source": pmc["source"] if pmc else None,
             "pmc_stale": pmc["stale"] if pmc else None,
         },
+        "results_ok_steps": starts_ok,
+        "step_latency": step_latency,
         "weak_matches": weak_matches,
         "faithful": faithful,
         "kernel_saturated": kernel,

@@ -1643,6 +1643,25 @@ int fr_export_bool_device(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_d
         dev.slots_to_device(slots.data(), n, dev_dst);
     })
 }
+int fr_export_bool_device_async(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst) {
+    FR_TRY({
+        NEED(ctx && (h || !n) && (dev_dst || !n));
+        if (n > 16) throw Error(FR_ERR_INVALID, "fr_export_bool_device_async: at most 16 handles");
+        std::vector<int> slots(n);
+        for (size_t i = 0; i < n; ++i) {
+            const HandleRec& r = ctx->get(h[i]);
+            if (r.b[0].slot < 0) return fr_export_bool_device(ctx, h, n, dev_dst);  // trivial: synchronising path
+            slots[i] = r.b[0].slot;
+        }
+        ctx->device().slots_to_device_async(slots.data(), n, dev_dst);
+    })
+}
+int fr_stream(fr_ctx* ctx, void** stream) {
+    FR_TRY({
+        NEED(ctx && stream);
+        *stream = ctx->device().stream();
+    })
+}
 int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct* out) {
     FR_TRY({
         NEED(ctx && out && (dev_src || !n));

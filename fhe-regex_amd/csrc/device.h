@@ -76,6 +76,10 @@ class Device {
     // buffer owned by the caller; both synchronise the library's stream on return
     void slots_to_device(const int* slots, size_t n, uint64_t* dst);
     void device_to_slots(const int* slots, size_t n, const uint64_t* src);
+    // stream-ordered slots_to_device for n <= 16 (the slot list travels as a kernel
+    // argument): returns once enqueued; order other streams after it with an event on stream()
+    void slots_to_device_async(const int* slots, size_t n, uint64_t* dst);
+    void* stream() const { return stream_; }
     void zero_slot(int slot);
 
     // run one dependency level of gates (all independent), async on the stream

@@ -1377,6 +1377,26 @@ __global__ void __launch_bounds__(256) k_buf_to_slots(const uint64_t* __restrict
     uint64_t* d = arena + (size_t)slots[blockIdx.x] * stride;
     for (int c = threadIdx.x; c < len; c += 256) d[c] = s[c];
 }
+struct SlotArgs {
+    int s[16];
+};
+__global__ void __launch_bounds__(256) k_slots_to_buf_arg(const uint64_t* __restrict__ arena, int stride, SlotArgs sl,
+                                                          int len, uint64_t* __restrict__ buf) {
+    const uint64_t* s = arena + (size_t)sl.s[blockIdx.x] * stride;
+    uint64_t* d = buf + (size_t)blockIdx.x * len;
+    for (int c = threadIdx.x; c < len; c += 256) d[c] = s[c];
+}
+void Device::slots_to_device_async(const int* slots, size_t n, uint64_t* dst) {
+    if (!n) return;
+    if (n > 16) throw Error(FR_ERR_INVALID, "slots_to_device_async: at most 16 slots");
+    SlotArgs a{};
+    for (size_t i = 0; i < n; ++i) {
+        if (slots[i] < 0 || (size_t)slots[i] >= next_slot_) throw Error(FR_ERR_INVALID, "slot list: slot out of range");
+        a.s[i] = slots[i];
+    }
+    k_slots_to_buf_arg<<<(unsigned)n, 256, 0, STREAM>>>(d_arena_, p_.slot_stride(), a, p_.lwe_len(), dst);
+    HIP_CHECK(hipGetLastError());
+}
 void Device::stage_slot_list(const int* slots, size_t n) {
     for (size_t i = 0; i < n; ++i)
         if (slots[i] < 0 || (size_t)slots[i] >= next_slot_) throw Error(FR_ERR_INVALID, "slot list: slot out of range");

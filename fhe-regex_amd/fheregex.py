@@ -166,6 +166,8 @@ _SIGS = {
     "fr_device_info": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
     "fr_debug_scalar": (C.c_uint64, [C.c_int32, C.c_uint64, C.c_uint64]),
     "fr_export_bool_device": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p]),
+    "fr_export_bool_device_async": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_void_p]),
+    "fr_stream": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p)]),
     "fr_import_bool_device": (C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t, C.POINTER(C.c_uint32)]),
     "fr_device_timers": (C.c_int, [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_uint64),
                                    C.POINTER(C.c_uint64)]),
@@ -442,6 +444,21 @@ class Context:
         _check(lib().fr_or_many(self.h, arr, len(hs), C.byref(out)))
         return out.value
 
+    def or_each(self, groups: Sequence[Sequence[int]]) -> List[int]:
+        """one OR per group of <= 16 booleans, all groups in one launch (fr_run_gates:
+        independent sign gates, the threshold OR of fr_or_many): the final bitor of
+        many start-sharded matches at once"""
+        gates = []
+        for grp in groups:
+            if not 1 <= len(grp) <= 16:
+                raise ValueError("or_each: 1..16 booleans per group")
+            g = Gate()
+            g.n_in, g.offset, g.kind = len(grp), -1, GATE_SIGN
+            for q, h in enumerate(grp):
+                g.in_[q], g.in_block[q], g.in_w[q] = h, 0, 1
+            gates.append(g)
+        return self.run_gates(gates) if gates else []
+
     def run_gates(self, gates: Sequence[Gate]) -> List[int]:
         arr = (Gate * len(gates))(*gates)
         _check(lib().fr_run_gates(self.h, arr, len(gates)))
@@ -483,6 +500,18 @@ class Context:
     def export_bool_device(self, hs: Sequence[int], dev_ptr: int):
         arr = (C.c_uint32 * len(hs))(*hs)
         _check(lib().fr_export_bool_device(self.h, arr, len(hs), C.c_void_p(dev_ptr)))
+
+    def export_bool_device_async(self, hs: Sequence[int], dev_ptr: int):
+        """stream-ordered export (no synchronisation): order other streams after it with
+        an event on stream_ptr()"""
+        arr = (C.c_uint32 * len(hs))(*hs)
+        _check(lib().fr_export_bool_device_async(self.h, arr, len(hs), C.c_void_p(dev_ptr)))
+
+    def stream_ptr(self) -> int:
+        """the context's hipStream_t (for torch.cuda.ExternalStream)"""
+        s = C.c_void_p()
+        _check(lib().fr_stream(self.h, C.byref(s)))
+        return s.value or 0
 
     def import_bool_device(self, dev_ptr: int, n: int) -> List[int]:
         out = (C.c_uint32 * n)()

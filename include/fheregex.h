@@ -235,6 +235,15 @@ int fr_plan_cache_stats(fr_ctx* ctx, uint64_t* entries, uint64_t* slots, uint64_
  * synchronise the library's stream before returning. */
 int fr_export_bool_device(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst);
 int fr_import_bool_device(fr_ctx* ctx, const uint64_t* dev_src, size_t n, fr_ct* out);
+/* Stream-ordered export (n <= 16): enqueued on the library's stream (fr_stream) after
+ * every earlier operation of the context, returns without synchronising; a caller
+ * orders its own stream after it with an event (e.g. the RCCL all-gather of the
+ * start-offset shards, which then never blocks the host between matches).  Handles
+ * with a trivial block 0 take the synchronising path. */
+int fr_export_bool_device_async(fr_ctx* ctx, const fr_ct* h, size_t n, uint64_t* dev_dst);
+/* The context's HIP stream (hipStream_t): every device operation of the context is
+ * ordered on it. */
+int fr_stream(fr_ctx* ctx, void** stream);
 /* Accumulated kernel timers of the profiling mode (fr_set_profiling): blind
  * rotation and (level 2) keyswitch milliseconds, launches and bootstraps. */
 int fr_device_timers(fr_ctx* ctx, double* br_ms, double* ks_ms, uint64_t* br_launches, uint64_t* br_gates);

@@ -26,8 +26,8 @@ def test_gpus_spawns_ranks(n):
     res = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--spawn-probe"], capture_output=True, text=True,
                          timeout=240, env=_env())
     assert res.returncode == 0, res.stderr[-2000:]
-    lines = [l for l in res.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, res.stdout  # one JSON line, from rank 0
+    lines = res.stdout.splitlines()
+    assert len(lines) == 1 and lines[0].startswith("{"), res.stdout  # one JSON line, from rank 0, nothing else
     d = json.loads(lines[0])
     assert d["spawn_probe"] and d["n_gpus"] == n and d["ranks"] == list(range(n))
     assert len(set(d["pids"])) == n

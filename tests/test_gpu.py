@@ -920,3 +920,30 @@ def test_start_shards_two_contexts_config4(gctx, key_blob, world, where):
         gctx.release(h)
     for c in ctxs[1:]:
         c.close()
+
+
+def test_export_async_and_or_each(gctx):
+    """The bench's start-shard pipeline pieces: a stream-ordered export right after an
+    asynchronous match (no synchronisation in between) writes the same words as the
+    synchronising export; or_each ORs groups in one launch like or_many."""
+    import torch
+    hs1 = gctx.upload_radix(gctx.encrypt_str("zzabczzzzz", seed=90))
+    hs0 = gctx.upload_radix(gctx.encrypt_str("zzzzzzzzzz", seed=91))
+    buf = torch.zeros((4, gctx.lwe_len), dtype=torch.int64, device="cuda:0")
+    outs = []
+    for i, hs in enumerate([hs1, hs0, hs0, hs1]):
+        o, _ = gctx.has_match(hs, "/abc/")
+        gctx.export_bool_device_async([o], buf[i].data_ptr())
+        outs.append(o)
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.ExternalStream(gctx.stream_ptr(), device=torch.device("cuda", 0)))
+    ev.synchronize()
+    ref = torch.zeros_like(buf)
+    gctx.export_bool_device(outs, ref.data_ptr())
+    assert torch.equal(buf, ref)
+    parts = gctx.import_bool_device(buf.data_ptr(), 4)
+    res = gctx.or_each([parts[:2], parts[1:3], parts[2:], [parts[3]]])
+    assert [gctx.decrypt_radix(gctx.download_radix(r)) for r in res] == [1, 0, 1, 1]
+    assert np.array_equal(gctx.download_radix(res[0]), gctx.download_radix(gctx.or_many(parts[:2])))
+    for h in hs1 + hs0 + outs + parts + res:
+        gctx.release(h)
