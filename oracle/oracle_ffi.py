@@ -15,7 +15,20 @@ import subprocess
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "build", "liboracle.so")
+LIB_PATH = os.path.join(HERE, "build", "liboracle.so")  # x86-64-v3 (AVX2 + FMA)
+LIB_PATH_V2 = os.path.join(HERE, "build", "liboracle_v2.so")  # the same source for CPUs without FMA
+
+
+def _cpu_has_fma() -> bool:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("flags"):
+                    fl = set(line.split(":", 1)[1].split())
+                    return {"fma", "avx2"} <= fl
+    except OSError:
+        pass
+    return False
 Q_RING = 998244353 * 1004535809  # GLWE/GGSW ring modulus (RNS: two NTT primes)
 RNS_PRIMES = (998244353, 1004535809)
 
@@ -52,9 +65,10 @@ _lib = None
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
+        path = LIB_PATH if _cpu_has_fma() else LIB_PATH_V2
+        if not os.path.exists(path):
             build()
-        L = C.CDLL(LIB_PATH)
+        L = C.CDLL(path)
         u64p = C.POINTER(C.c_uint64)
         L.or_q_mul.restype = C.c_uint64
         L.or_q_mul.argtypes = [C.c_uint64, C.c_uint64]
