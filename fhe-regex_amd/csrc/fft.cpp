@@ -87,7 +87,7 @@ void bsk_to_fourier(const Tables& T, const std::vector<uint64_t>& bsk, size_t po
     const int N = T.N, M = T.M;
     if (bsk.size() != polys * (size_t)N) throw Error(FR_ERR_INVALID, "bsk_to_fourier: size");
     out.resize(polys * (size_t)M);
-    const double scale = std::ldexp(1.0, -T.LOG);
+    const double scale = fourier_key_scale(T.LOG);  // 1/M and the accumulator unit (fft.h), exact
     unsigned hw = std::thread::hardware_concurrency();
     const size_t nt = hw ? (hw > 16 ? 16 : hw) : 4;
     std::vector<std::thread> th;

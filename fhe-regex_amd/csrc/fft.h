@@ -128,26 +128,48 @@ FR_HD uint64_t torus_of(double v) {
     const double lo = FR_FMA(-hi, 0x1p32, ri);
     return ((uint64_t)(uint32_t)hm << 32) | (uint64_t)(uint32_t)lo;
 }
-// The blind rotation's accumulator is f64: a torus value t (mod 2^64) is held as a
-// double in [-2^63, 2^63] congruent to t up to the rounding of the additions (below
-// 2^44 per step, far under the bootstrap noise).  Per step:
-//   digit  d = rint(a 2^-(64-B)) in [-2^(B-1), 2^(B-1)] (one level, base 2^B: the
-//          closest multiple of 2^(64-B), ties to even)
-//   update a = reduce(a + v), v the inverse transform's f64 output (|v| < 2^100),
-//          reduce(a) = fma(-rint(a 2^-64), 2^64, a), exact
-// and torus_of(a) gives the u64 torus value for sample extraction.
+// The blind rotation's accumulator is f64: a torus value a (mod 2^64) is held as
+// t = a 2^-ACC_LOG, a double in [-2^22, 2^22] (ACC_LOG = 41 = 64 - B for the one-level
+// gadget base 2^B = 2^23) congruent to a 2^-ACC_LOG up to the rounding of the additions
+// (below 2^44 2^-ACC_LOG per step, far under the bootstrap noise).  The
+// Fourier key carries the same 2^-ACC_LOG (with the transform's 1/M), so every product
+// and sum of a step is the unscaled computation times an exact power of two: the same
+// mantissas, the same roundings (no value comes near the f64 range limits).  Per step:
+//   digit  d = rint(t) in [-2^(B-1), 2^(B-1)] (the closest multiple of 2^(64-B) of a,
+//          ties to even)
+//   update t = reduce(t + v), v the inverse transform's f64 output (|v| < 2^59),
+//          reduce(t) = fma(-rint(t 2^-B), 2^B, t), exact
+// and torus_of(t 2^ACC_LOG) gives the u64 torus value for sample extraction.
+// (Round 3 held a itself: digit rint(a 2^-41), reduce by 2^64; the scaled form saves the
+// digit's multiply, 8 VALU per lane and step of the latency shape.)
 #if defined(__HIPCC__)
 #define FR_RINT(x) __builtin_rint(x)
 #else
 #define FR_RINT(x) std::nearbyint(x)
 #endif
+constexpr int ACC_LOG = 41;
 template <int B>
-FR_HD double acc_digit(double a) {
-    return FR_RINT(a * (1.0 / (double)(1ULL << (64 - B))));
+FR_HD double acc_digit(double t) {
+    static_assert(B == 64 - ACC_LOG, "the accumulator unit is the gadget's 2^(64-B)");
+    return FR_RINT(t);
 }
-FR_HD double acc_reduce(double a) { return FR_FMA(-FR_RINT(a * 0x1p-64), 0x1p64, a); }
-// exact f64 of a u64 torus value, as the signed representative in [-2^63, 2^63)
-FR_HD double acc_of_torus(uint64_t t) { return (double)(int64_t)t; }
+template <int B>
+FR_HD double acc_reduce(double t) {
+    static_assert(B == 64 - ACC_LOG, "the accumulator unit is the gadget's 2^(64-B)");
+    return FR_FMA(-FR_RINT(t * (1.0 / (double)(1ULL << B))), (double)(1ULL << B), t);
+}
+// exact f64 of a u64 torus value (signed representative in [-2^63, 2^63)), in accumulator units
+FR_HD double acc_of_torus(uint64_t u) { return (double)(int64_t)u * 0x1p-41; }
+// the u64 torus value of an accumulator entry
+FR_HD uint64_t torus_of_acc(double t) { return torus_of(t * 0x1p41); }
+// scale of the Fourier bootstrapping key: the inverse transform's 1/M and the accumulator unit
+FR_HD double fourier_key_scale(int log2M) {
+#if defined(__HIPCC__)
+    return __builtin_ldexp(1.0, -(log2M + ACC_LOG));
+#else
+    return std::ldexp(1.0, -(log2M + ACC_LOG));
+#endif
+}
 
 // ---------------------------------------------------------------- host side
 // psi^x (x mod 2N) = i^q (cos(pi r / N), sin(pi r / N)), x = q N/2 + r
@@ -164,8 +186,8 @@ struct Tables {
 };
 
 // Fourier bootstrapping key: every GGSW polynomial of the torus BSK
-// ([w][r][c][coef] u64) folded, transformed and scaled by 1/M, as
-// [w][r][c][slot] complex.
+// ([w][r][c][coef] u64) folded, transformed and scaled by fourier_key_scale (1/M and the
+// accumulator unit 2^-ACC_LOG), as [w][r][c][slot] complex.
 void bsk_to_fourier(const Tables& T, const std::vector<uint64_t>& bsk, size_t polys, std::vector<c64>& out);
 
 }  // namespace fft

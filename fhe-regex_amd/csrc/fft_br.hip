@@ -973,8 +973,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         for (int b = 0; b < B; ++b)
 #pragma unroll
             for (int m = 0; m < E; ++m) {
-                alo[b][m] = fft::acc_reduce(alo[b][m] + x[b][m].x);
-                ahi[b][m] = fft::acc_reduce(ahi[b][m] + x[b][m].y);
+                alo[b][m] = fft::acc_reduce<23>(alo[b][m] + x[b][m].x);
+                ahi[b][m] = fft::acc_reduce<23>(ahi[b][m] + x[b][m].y);
             }
         FBR_STAMP(5);
     }
@@ -996,8 +996,8 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
         for (int m = 0; m < E; ++m) {
             const int j = G::template idx<0>(tl, m);
-            accs[(b * (K + 1) + P) * N + j] = fft::torus_of(alo[b][m]);
-            accs[(b * (K + 1) + P) * N + j + M] = fft::torus_of(ahi[b][m]);
+            accs[(b * (K + 1) + P) * N + j] = fft::torus_of_acc(alo[b][m]);
+            accs[(b * (K + 1) + P) * N + j + M] = fft::torus_of_acc(ahi[b][m]);
         }
     static_assert(B == 1 || 8 * B * (K + 1) * N <= 16 * B * BS, "pair shape: u64 rows inside the forward rows");
 #pragma unroll

@@ -141,7 +141,7 @@ __device__ __forceinline__ int lane_slot(int tl, int m) {
     constexpr int LOG = __builtin_ctz(M), e = __builtin_ctz(E), LAST = (LOG + e - 1) / e - 1;
     return geo_base(LOG, e, LAST, tl, fft_layout_variant(LOG, e)) + (m << geo_lo(LOG, e, LAST));
 }
-// fold + forward FFT + 1/M of one polynomial, written in the lane layouts of
+// fold + forward FFT + fourier_key_scale of one polynomial, written in the lane layouts of
 // the E = 4, 8 and 16 kernels ([poly][m][lane], slot of (lane, m) per geo.h; a null
 // output is skipped)
 template <int N>
@@ -168,7 +168,7 @@ __global__ void __launch_bounds__(256) k_bsk_fourier(const uint64_t* __restrict_
         }
         __syncthreads();
     }
-    const double scale = 1.0 / (double)M;  // 2^-LOG, exact
+    const double scale = fft::fourier_key_scale(LOG);  // 1/M and the accumulator unit (fft.h), exact
     for (int idx = tid; idx < M; idx += 256) {
         if (out4) {
             const double2 v = z[lane_slot<M, 4>(idx % (M / 4), idx / (M / 4))];
