@@ -347,7 +347,7 @@ def main():
     ap.add_argument("--probe", default="1,16,254",
                     help="comma-separated batch sizes: blind-rotation ms per launch vs batch ('' to skip)")
     ap.add_argument("--pmc", default="",
-                    help="PMC summary of the BR kernel (tools/pmc_summary.py); default: profiles/r03/"
+                    help="PMC summary of the BR kernel (tools/pmc_summary.py); default: the newest profiles/r0N/"
                          "pmc_summary.json at k1n2048, pmc_summary_k2n1024.json at k2n1024")
     args = ap.parse_args()
     if args.gpus < 1:
@@ -360,9 +360,10 @@ def main():
     if args.spawn_probe:
         spawn_probe(int(env_world or 1), int(os.environ.get("RANK", "0")))
         return
-    if not args.pmc:
-        args.pmc = os.path.join(REPO, "profiles", "r03",
-                                "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json")
+    if not args.pmc:  # the newest round's PMC summary of this parameter point
+        name = "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json"
+        cands = [os.path.join(REPO, "profiles", r, name) for r in ("r04", "r03")]
+        args.pmc = next((c for c in cands if os.path.exists(c)), cands[-1])
     if args.matches < 1:
         ap.error("--matches must be >= 1")
 
