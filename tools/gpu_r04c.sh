@@ -12,7 +12,8 @@ tail -2 "$out/gpu_tests.log"
 step 200 python __graft_entry__.py smoke > "$out/smoke.log" 2>&1 || { cat "$out/smoke.log"; exit 1; }
 tail -1 "$out/smoke.log"
 if [ -n "$A" ]; then
-  SIZES="1 16 254 512 2048" step 600 bash tools/ab_libs.sh 3 "$A" "$B" > "$out/ab.log" 2>&1 || { cat "$out/ab.log"; exit 1; }
+  shift 1
+  step 900 bash tools/ab_r04.sh 3 "$@" > "$out/ab.log" 2>&1 || { cat "$out/ab.log"; exit 1; }
   cat "$out/ab.log"
 fi
 step 400 python3 bench.py --steps 20 --warmup 5 > "$out/bench.json" 2> "$out/bench.err" || { tail -20 "$out/bench.err"; exit 1; }
