@@ -710,6 +710,7 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
     cplx* D = malloc(sizeof(cplx) * kp1 * M);
     cplx* Z = malloc(sizeof(cplx) * M);
     uint64_t* V = malloc(8 * N);
+    struct { double cr[3], ci[3]; }* SF = malloc(sizeof(*SF) * M); /* a step's slot factors */
     const uint64_t delta = 1ULL << 59;
     if (direct == 1) {
         int box = N / 16, half = box / 2;
@@ -735,17 +736,22 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
             }
             fft_forward(F, Dc);
         }
+        /* slot factors: psi^(a_i L), psi^(a_j L) from the quadrant table, and their
+         * product for a_i + a_j (N is a power of two: masks and shifts, not divisions) */
+        const uint32_t m2N = 2u * (uint32_t)N - 1u, mq = (uint32_t)(N / 2) - 1u;
+        const int lq = ilog2(N / 2);
+        for (int t = 0; t < M; t++) {
+            for (int h = 1; h < 3; h++) {
+                uint32_t kk = (uint32_t)((uint64_t)(h == 1 ? ai : aj) * F->leaf[t]) & m2N;
+                cplx qv = F->qt[kk & mq];
+                quarter_turns(qv.re, qv.im, kk >> lq, &SF[t].cr[h], &SF[t].ci[h]);
+            }
+            c_mul(SF[t].cr[1], SF[t].ci[1], SF[t].cr[2], SF[t].ci[2], &SF[t].cr[0], &SF[t].ci[0]);
+        }
         for (size_t c = 0; c < kp1; c++) {
             for (int t = 0; t < M; t++) {
-                /* slot factors: psi^(a_i L), psi^(a_j L) from the quadrant table, and
-                 * their product for a_i + a_j */
-                double cr[3], ci[3];
-                for (int h = 1; h < 3; h++) {
-                    uint32_t kk = (uint32_t)(((uint64_t)(h == 1 ? ai : aj) * F->leaf[t]) % (2 * (uint64_t)N));
-                    cplx qv = F->qt[kk % (uint32_t)(N / 2)];
-                    quarter_turns(qv.re, qv.im, kk / (uint32_t)(N / 2), &cr[h], &ci[h]);
-                }
-                c_mul(cr[1], ci[1], cr[2], ci[2], &cr[0], &ci[0]);
+                const double* cr = SF[t].cr;
+                const double* ci = SF[t].ci;
                 /* per row r: K_r = sum_g G_g[r][c] (c_g - 1), g ascending; then
                  * z = D_c K_c + sum_(r != c, ascending) D_r K_r (the r = c term first) */
                 double kr[8], ki[8]; /* k + 1 <= 8 (or_bsk_prepare) */
@@ -791,7 +797,7 @@ static void blind_rotate_torus(or_bsk* K, const uint64_t* ks_lwe, const uint8_t*
         }
         if (direct == 2) out[big] += 1ULL << 58;
     }
-    free(acc); free(dacc); free(D); free(Z); free(V);
+    free(acc); free(dacc); free(D); free(Z); free(V); free(SF);
 }
 
 void or_blind_rotate_multi(void* pk, const uint64_t* ks_lwe, const uint8_t* luts, int n_out, int direct, uint64_t* outs) {
