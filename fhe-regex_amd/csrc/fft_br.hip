@@ -190,6 +190,33 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 //    SIMD), against 1.34: nine exchanges per transform, three of them cross-wave
 //    (ab_lat_e2_16wave.log).
 
+// The twiddles of phase p are wave-uniform when every lane of a wave reads the same table
+// entry for each of the phase's stages (the index bits the entry depends on sit on element or
+// wave bits of that layout: phases 0 and 1 of the k = 1 geometry).  Those stay in SGPRs, which
+// frees 4 VGPRs per complex twiddle (pair shape: 16 of its 256, where it spilled 16).
+template <int M, int E, int p>
+constexpr bool ftw_wave_uniform() {
+    using G = FGeo<M, E>;
+    for (int w = 0; w * 64 < G::T; ++w)
+        for (int s = G::s_begin(p); s < G::s_end(p); ++s) {
+            const int ref = geo_base(G::LOG, G::e, p, w * 64, FV<M, E>) >> (G::LOG - s);
+            for (int l = 1; l < 64; ++l)
+                if ((geo_base(G::LOG, G::e, p, w * 64 + l, FV<M, E>) >> (G::LOG - s)) != ref) return false;
+        }
+    return true;
+}
+__device__ __forceinline__ double2 fwave_uniform(double2 v) {
+    const unsigned long long a = (unsigned long long)__double_as_longlong(v.x);
+    const unsigned long long b = (unsigned long long)__double_as_longlong(v.y);
+    const unsigned a0 = __builtin_amdgcn_readfirstlane((unsigned)a), a1 = __builtin_amdgcn_readfirstlane((unsigned)(a >> 32));
+    const unsigned b0 = __builtin_amdgcn_readfirstlane((unsigned)b), b1 = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+    return make_double2(__longlong_as_double((long long)(((unsigned long long)a1 << 32) | a0)),
+                        __longlong_as_double((long long)(((unsigned long long)b1 << 32) | b0)));
+}
+#ifndef FR_TW_SGPR
+#define FR_TW_SGPR 1
+#endif
+
 template <int M, int E>
 constexpr int ftw_index(int s, int m) {
     const int d = FGeo<M, E>::LOG - 1 - s - FGeo<M, E>::lo(s / FGeo<M, E>::e);
@@ -202,6 +229,11 @@ __device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* t
         double2 c, ca, cc;
         ftw_r4<M, E, p>(tw, tl, c, ca);
         fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
+        if constexpr (FR_TW_SGPR && ftw_wave_uniform<M, E, p>()) {
+            c = fwave_uniform(c);
+            ca = fwave_uniform(ca);
+            cc = fwave_uniform(cc);
+        }
         twr.v[3 * p] = c, twr.v[3 * p + 1] = ca, twr.v[3 * p + 2] = cc;
         if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1>(twr, tw, tl);
         return;
