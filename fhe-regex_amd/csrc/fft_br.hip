@@ -420,6 +420,12 @@ __device__ __forceinline__ void fexchange(double2 (&x)[B][E], double2* row, int 
         double2* rf = row + G::template at<X>(G::template base<PF>(tl));
         double2* rt = row + G::template at<X>(G::template base<PT>(tl));
         if constexpr (PRE) __syncthreads();
+#ifdef FR_XCHG_PRIO  // A/B experiment: a wave entering an exchange issues ahead of its SIMD partner
+        __builtin_amdgcn_s_setprio(FR_XCHG_PRIO);
+        struct PrioReset {
+            __device__ ~PrioReset() { __builtin_amdgcn_s_setprio(0); }
+        } prio_reset;
+#endif
         if constexpr (XK && fxkeep_ok<M, E, PF, PT>()) {  // the kept element: wave-uniform branches around its store and load
             const int q = __builtin_amdgcn_readfirstlane((tl >> 6) & (E - 1));
 #pragma unroll
