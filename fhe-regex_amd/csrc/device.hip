@@ -857,35 +857,20 @@ k_ks_digits16(const DevGate* __restrict__ gates, int B, const uint64_t* __restri
             v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + big];
         ks[(size_t)g * ks_stride + ks_n] = v;
     }
-    // the inputs' rows, resolved once per workgroup (content references through the map)
-    __shared__ const ulonglong2* rows[16];
-    if (threadIdx.x < nin) rows[threadIdx.x] = (const ulonglong2*)(arena + (size_t)arena_slot(gg.in_slot[threadIdx.x], cmap) * slot_stride);
-    __syncthreads();
     for (int q = threadIdx.x; q < groups; q += blockDim.x) {
         uint64_t v[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) v[e] = 0;
-        // four inputs' loads in flight at once: a gate of fan-in 16 (an OR level) took 16 dependent
-        // rounds of L2 latency here, ~19 us for one gate against ~10 us for two-input gates
-        for (int q0 = 0; q0 < nin; q0 += 4) {
-            ulonglong2 x[4][8];
+        for (int qi = 0; qi < nin; ++qi) {
+            const uint64_t w = (uint64_t)(int64_t)gg.in_w[qi];
+            const ulonglong2* src =
+                (const ulonglong2*)(arena + (size_t)arena_slot(gg.in_slot[qi], cmap) * slot_stride + 16 * q);
 #pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (q0 + u < nin) {
-                    const ulonglong2* src = rows[q0 + u] + 8 * q;
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) x[u][e] = src[e];
-                }
-#pragma unroll
-            for (int u = 0; u < 4; ++u)
-                if (q0 + u < nin) {
-                    const uint64_t w = (uint64_t)(int64_t)gg.in_w[q0 + u];
-#pragma unroll
-                    for (int e = 0; e < 8; ++e) {
-                        v[2 * e] += w * x[u][e].x;
-                        v[2 * e + 1] += w * x[u][e].y;
-                    }
-                }
+            for (int e = 0; e < 8; ++e) {
+                const ulonglong2 x = src[e];
+                v[2 * e] += w * x.x;
+                v[2 * e + 1] += w * x.y;
+            }
         }
         uint32_t words[4 * KSL];
 #pragma unroll

@@ -213,8 +213,14 @@ __device__ __forceinline__ double2 fwave_uniform(double2 v) {
     return make_double2(__longlong_as_double((long long)(((unsigned long long)a1 << 32) | a0)),
                         __longlong_as_double((long long)(((unsigned long long)b1 << 32) | b0)));
 }
-#ifndef FR_TW_SGPR
-#define FR_TW_SGPR 1
+// Measured (profiles/r04/ab_r04c.log): the pair shape gains (512 bootstraps 2.62-2.69 -> 2.53-2.56 ms,
+// its 16 spilled VGPRs gone); the latency shape lost 5% (one bootstrap 1.31 -> 1.38 ms, a worse
+// schedule at 190 VGPRs), so it keeps the twiddles in VGPRs
+#ifndef FR_TW_SGPR_PAIR
+#define FR_TW_SGPR_PAIR 1
+#endif
+#ifndef FR_TW_SGPR_LAT
+#define FR_TW_SGPR_LAT 0
 #endif
 
 template <int M, int E>
@@ -222,20 +228,20 @@ constexpr int ftw_index(int s, int m) {
     const int d = FGeo<M, E>::LOG - 1 - s - FGeo<M, E>::lo(s / FGeo<M, E>::e);
     return s * (E / 2) + ((m >> (d + 1)) << d) + (m & ((1 << d) - 1));
 }
-template <int M, int E, int p>
+template <int M, int E, int p, bool UNI = false>
 __device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* tw, int tl) {
     using G = FGeo<M, E>;
     if constexpr (fradix4<M, E>()) {
         double2 c, ca, cc;
         ftw_r4<M, E, p>(tw, tl, c, ca);
         fft::cmul(c.x, c.y, ca.x, ca.y, cc.x, cc.y);
-        if constexpr (FR_TW_SGPR && ftw_wave_uniform<M, E, p>()) {
+        if constexpr (UNI && ftw_wave_uniform<M, E, p>()) {
             c = fwave_uniform(c);
             ca = fwave_uniform(ca);
             cc = fwave_uniform(cc);
         }
         twr.v[3 * p] = c, twr.v[3 * p + 1] = ca, twr.v[3 * p + 2] = cc;
-        if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1>(twr, tw, tl);
+        if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1, UNI>(twr, tw, tl);
         return;
     }
     const int b = G::template base<p>(tl);
@@ -249,7 +255,7 @@ __device__ __forceinline__ void ftw_load_phase(FTwr<M, E>& twr, const double2* t
             twr.v[ftw_index<M, E>(s, m)] = zs[(1 << s) + (G::template moff<p>(m) >> (G::LOG - s))];
         }
     }
-    if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1>(twr, tw, tl);
+    if constexpr (p + 1 < G::NPH) ftw_load_phase<M, E, p + 1, UNI>(twr, tw, tl);
 }
 template <int M, int E, int p>
 __device__ __forceinline__ void ffwd_phase_r(double2 (&x)[E], const FTwr<M, E>& twr) {
@@ -778,7 +784,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     // and (k = 1) the lane's twiddles
     double2 gv[3][K + 1][LAT ? E : 1];
     FTwr<M, TWR ? E : 2> twr;
-    if constexpr (TWR) ftw_load_phase<M, E, 0>(twr, B == 1 ? tw : tw_g, tl);
+    if constexpr (TWR) ftw_load_phase<M, E, 0, B == 1 ? FR_TW_SGPR_LAT : FR_TW_SGPR_PAIR>(twr, B == 1 ? tw : tw_g, tl);
 #ifdef FR_BR_TIMING
     uint64_t tseg[6] = {0, 0, 0, 0, 0, 0};
     uint64_t tlast = __builtin_amdgcn_s_memtime();
