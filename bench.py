@@ -238,7 +238,11 @@ def pmc_figures(params, path: str):
     src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
     sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16] if os.path.exists(src) else None
     shapes = {}
-    for ln in d.get("launches", []):
+    lns = d.get("launches", [])
+    sat_grid = max((ln.get("grid", 0) for ln in lns), default=None)  # the saturated probe (as pmc_summary.py)
+    for ln in lns:
+        if ln.get("grid") == sat_grid:
+            continue
         m = re.search(r"<\s*\d+,\s*\d+,\s*\d+,\s*(true|false),\s*(\d+)\s*>", ln.get("kernel", ""))
         if not m or not ln.get("calls"):
             continue
