@@ -947,3 +947,25 @@ def test_export_async_and_or_each(gctx):
     assert np.array_equal(gctx.download_radix(res[0]), gctx.download_radix(gctx.or_many(parts[:2])))
     for h in hs1 + hs0 + outs + parts + res:
         gctx.release(h)
+
+
+@pytest.mark.parametrize("which", ["metric", "config3", "config4", "config5"])
+def test_match_words_full_size_configs(gctx, oracle_k1, which):
+    """Whole BASELINE workloads at their full sizes, word for word against the oracle's
+    evaluation of the same schedule on the same LWEs: /abc/ x 256 (783 rotations), config 3
+    as written under the grammar extension (785), config 4 /the/i x 1024 (3,139 rotations, 5
+    levels) and config 5 on 512 chars through the merged engine (1,817 rotations, 9 levels)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    pat, kind, L = {"metric": ("/abc/", "printable", 256), "config3": ("/^[a-z0-9]+$/", "alnum", 256),
+                    "config4": ("/the/i", "letters", 1024), "config5": (bench.CONFIG5, "config5", 512)}[which]
+    content = bench.make_content(kind, L, seed=3).decode()
+    grammar = F.GRAMMAR_EXT if which == "config3" else F.GRAMMAR_REFERENCE
+    gctx.set_grammar(grammar)
+    try:
+        got = _match_words_vs_oracle(gctx, oracle_k1, content, pat, 4000 + L, grammar=grammar)
+    finally:
+        gctx.set_grammar(F.GRAMMAR_REFERENCE)
+    exp = ro.has_match_reach(content, pat, ext=True) if which == "config3" else ro.has_match_reach(content, pat)
+    assert got == exp == 1
