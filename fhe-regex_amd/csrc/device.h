@@ -179,6 +179,7 @@ class Device {
     // k = 1: larger launches up to this many use the pair shape (2 per workgroup; every size
     // by default: profiles/r03/ab_pair_shape.log)
     size_t fft_pair_ = SIZE_MAX;
+    bool fft_dual_ = false;  // FR_FFT_DUAL=1: the dual shape instead of the pair (experiment)
     // Fourier BSK, one copy per lane geometry in use: [0] E = 4 (latency shape, always),
     // [1] E = 8, [2] E = 16 (the throughput shape's when fft_e_ is that)
     double* d_fbsk_[3] = {nullptr, nullptr, nullptr};

@@ -1089,6 +1089,216 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     }
 }
 
+// Dual shape (round 4 experiment, k = 1, FR_FFT_DUAL=1): one bootstrap per workgroup on
+// M / E = 256 lanes (4 waves), each lane holding the same slots of BOTH polynomials
+// (x[P][E]: the pair shape's B dimension carries the polynomial), two workgroups per CU.
+// Both digit polynomials of a slot are in the lane, so the MAC needs no exchange and no
+// barrier: the lane computes both output columns from all four (r, c) key values of its
+// slots (the same operation sequence per output as the other shapes: bit-identical).  The
+// forward and inverse share one row set (pre-barriers, as the throughput shape: 4 barriers
+// per step), 54 KB of LDS per workgroup.  Each workgroup streams the whole key (the pair
+// shape shares it between two bootstraps); the two workgroups of a CU have their own
+// barriers, so one computes while the other waits.
+template <int N>
+constexpr size_t fbr_dual_smem_bytes() {
+    return 16 * (2 * (size_t)FGeo<N / 2, 4>::NP + (size_t)N / 2) + 16 * MAX_OUT + 2 * 1026 + 4 * 16 * MAX_OUT +
+           4 * MAX_OUT;
+}
+template <int N>
+__global__ void __launch_bounds__(N / 8, 2)
+k_blind_rotate_fft_dual(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
+                        int n_gates, const double2* __restrict__ bsk, const double2* __restrict__ tw_g,
+                        const double2* __restrict__ psi_g, const uint16_t* __restrict__ leaf_g,
+                        uint64_t* __restrict__ arena, int slot_stride) {
+    constexpr int K = 1, E = 4, M = N / 2, B = 2;
+    using G = FGeo<M, E>;
+    static_assert(fexchanges_conflict_free<M, E>(), "LDS maps must make every exchange conflict-free");
+    static_assert(fradix4<M, E>(), "dual shape: the k = 1 geometry (radix-4 inverse)");
+    constexpr int T = M / E, NT = T, LAST = G::NPH - 1;
+    constexpr int LOG2N2 = G::LOG + 2;
+    constexpr int BS = G::NP;  // polynomial P's exchange row at P BS
+    extern __shared__ __attribute__((aligned(16))) double2 fsm[];
+    double2* xbuf = fsm;
+    double2* psi = xbuf + B * BS;  // quadrant table psi^k, k < N/2
+    uint8_t* lut = (uint8_t*)(psi + N / 2);
+    uint16_t* abar = (uint16_t*)(lut + 16 * MAX_OUT);
+    uint32_t* wterms = (uint32_t*)(abar + 1026);
+    int* wcnt = (int*)(wterms + 16 * MAX_OUT);
+
+    const int tl = threadIdx.x;
+    const int gi = (int)blockIdx.x;
+    const uint64_t* in = ks + (size_t)gi * ks_stride;
+    const int n_out = gates[gi].n_out, kind = gates[gi].direct;
+    for (int i = tl; i < N / 2; i += NT) psi[psi_slot(i)] = psi_g[i];
+    for (int i = tl; i < 16 * n_out; i += NT) lut[i] = gates[gi].lut[i / 16][i % 16];
+    for (int i = tl; i < n; i += NT) abar[i] = (uint16_t)mod_switch(in[i], LOG2N2);
+    if (tl == 0) abar[n] = 0;
+    const uint32_t bbar = mod_switch(in[n], LOG2N2);
+    const uint32_t Lb = (1u + 4u * (__brev((uint32_t)G::template idx<LAST>(tl, 0)) >> (32 - G::LOG))) & (uint32_t)(M - 1);
+    __syncthreads();
+
+    double alo[B][E], ahi[B][E];
+    {
+        const bool direct = kind == JOB_DIRECT;
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            uint64_t v[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int s = (j + h * M + (int)bbar) & (2 * N - 1);
+                const uint64_t tv = test_poly<N>(s & (N - 1), direct, lut);
+                v[h] = s < N ? tv : (uint64_t)0 - tv;
+            }
+#pragma unroll
+            for (int P = 0; P < B; ++P) {
+                alo[P][m] = P == K ? fft::acc_of_torus(v[0]) : 0.0;
+                ahi[P][m] = P == K ? fft::acc_of_torus(v[1]) : 0.0;
+            }
+        }
+    }
+    constexpr uint32_t GG = (uint32_t)(K + 1) * (K + 1) * M;
+    const __amdgpu_buffer_rsrc_t rs = bsk_rsrc(bsk);
+    const uint32_t lane_off = 16u * (uint32_t)tl;
+    const int steps = (n + 1) / 2;
+    FTwr<M, E> twr;
+    ftw_load_phase<M, E, 0, FR_TW_SGPR_PAIR>(twr, tw_g, tl);
+    // slot m's key values [g][r][c] (Fourier GGSW [r][c][m][lane])
+    auto load_keys = [&](double2 (&Bk)[3][2][2], uint32_t sbase, int m) {
+#pragma unroll
+        for (int gg = 0; gg < 3; ++gg)
+#pragma unroll
+            for (int r = 0; r < 2; ++r)
+#pragma unroll
+                for (int c = 0; c < 2; ++c)
+                    Bk[gg][r][c] =
+                        bsk_load(rs, lane_off, sbase + 16u * (gg * GG + (uint32_t)(r * 2 + c) * M + (uint32_t)m * T));
+    };
+    for (int t = 0; t < steps; ++t) {
+        if ((abar[2 * t] | abar[2 * t + 1]) == 0) continue;  // (uniform) X^0 acc - acc = 0
+        const uint32_t sbase = (uint32_t)__builtin_amdgcn_readfirstlane(t) * (3u * GG * 16u);
+        double2 Bc[3][2][2];
+        load_keys(Bc, sbase, 0);  // slot 0 lands during the digits and the forward FFT
+        const uint32_t ei = __builtin_amdgcn_readfirstlane((uint32_t)abar[2 * t]);
+        const uint32_t ej = __builtin_amdgcn_readfirstlane((uint32_t)abar[2 * t + 1]);
+        double2 x[B][E];
+#pragma unroll
+        for (int P = 0; P < B; ++P)
+#pragma unroll
+            for (int m = 0; m < E; ++m)
+                x[P][m] = make_double2(fft::acc_digit<23>(alo[P][m]), fft::acc_digit<23>(ahi[P][m]));
+        fforward_from<M, E, 0, false, true, B, BS>(x, xbuf, twr, nullptr, tl, [](auto) {});
+        // slot factors (quadrant table + quarter turns, as the pair shape)
+        double bre[2], bim[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t k = __umul24(h == 0 ? ei : ej, Lb) & (2 * N - 1);
+            const double2 q = psi[psi_slot((int)(k & (N / 2 - 1)))];
+            fft::psi_quadrant(q.x, q.y, k >> (LOG2N2 - 2), bre[h], bim[h]);
+        }
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            double2 Bn[3][2][2];
+            if (m + 1 < E) load_keys(Bn, sbase, m + 1);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
+            double cr[3], ci[3];
+#pragma unroll
+            for (int h = 1; h < 3; ++h) slot_factor(bre[h - 1], bim[h - 1], h == 1 ? ei : ej, sm, cr[h], ci[h]);
+            fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
+            double2 z[B];
+#pragma unroll
+            for (int c = 0; c < B; ++c) {  // output column c: K_r = sum_g B_g[r][c] (c_g - 1), own row first
+                double kor, koi, kxr, kxi;
+#pragma unroll
+                for (int gg = 0; gg < 3; ++gg) {
+                    const double c1r = cr[gg] - 1.0, c1i = ci[gg];
+                    const double2 Bo = Bc[gg][c][c], Bx = Bc[gg][1 - c][c];
+                    if (gg == 0) {
+                        fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                        fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr, kxi);
+                    } else {
+                        fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                        fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr, kxi);
+                    }
+                }
+                double zr, zi;
+                fft::cmul(x[c][m].x, x[c][m].y, kor, koi, zr, zi);
+                fft::cmac(x[1 - c][m].x, x[1 - c][m].y, kxr, kxi, zr, zi);
+                z[c] = make_double2(zr, zi);
+            }
+#pragma unroll
+            for (int c = 0; c < B; ++c) x[c][m] = z[c];
+            __builtin_amdgcn_sched_barrier(0);
+            if (m + 1 < E) {
+#pragma unroll
+                for (int gg = 0; gg < 3; ++gg)
+#pragma unroll
+                    for (int r = 0; r < 2; ++r)
+#pragma unroll
+                        for (int c = 0; c < 2; ++c) Bc[gg][r][c] = Bn[gg][r][c];
+            }
+        }
+        finverse_from<M, E, LAST, false, true, B, BS>(x, xbuf, twr, nullptr, nullptr, tl);
+#pragma unroll
+        for (int P = 0; P < B; ++P)
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                alo[P][m] = fft::acc_reduce<23>(alo[P][m] + x[P][m].x);
+                ahi[P][m] = fft::acc_reduce<23>(ahi[P][m] + x[P][m].y);
+            }
+    }
+
+    // publish the accumulator as u64 [P][N] over the rows, then sample extract / w-step
+    __syncthreads();
+    uint64_t* accs = (uint64_t*)xbuf;
+    static_assert(8 * B * N <= 16 * B * BS, "dual shape: u64 rows inside the exchange rows");
+#pragma unroll
+    for (int P = 0; P < B; ++P)
+#pragma unroll
+        for (int m = 0; m < E; ++m) {
+            const int j = G::template idx<0>(tl, m);
+            accs[P * N + j] = fft::torus_of_acc(alo[P][m]);
+            accs[P * N + j + M] = fft::torus_of_acc(ahi[P][m]);
+        }
+    if (tl < n_out && kind == JOB_MULTI) {
+        constexpr int box = N / 16, half = box / 2;
+        const uint8_t* lf = lut + 16 * tl;
+        uint32_t* terms = wterms + 16 * tl;
+        int nt = 0;
+        for (int tt = 1; tt <= 16; ++tt) {
+            const int d = tt < 16 ? (int)lf[tt] - (int)lf[tt - 1] : -((int)lf[0] + (int)lf[15]);
+            if (d != 0) terms[nt++] = (uint32_t)(tt < 16 ? tt * box - half : N - half) | ((uint32_t)(d + 128) << 16);
+        }
+        wcnt[tl] = nt;
+    }
+    __syncthreads();
+    if (gi >= n_gates) return;
+    constexpr int big = K * N;
+    if (kind != JOB_MULTI) {
+        uint64_t* out = arena + (size_t)gates[gi].out_slot[0] * slot_stride;
+        const uint64_t post = kind == JOB_SIGN ? (1ULL << (DELTA_LOG - 1)) : 0;
+        for (int c = tl; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint64_t v = accs[pp * N + j];
+            out[c] = (t != 0 ? (uint64_t)0 - v : v) + (c == big ? post : 0);
+        }
+        return;
+    }
+    for (int f = 0; f < n_out; ++f) {
+        const uint32_t* tf = wterms + 16 * f;
+        const int nt = wcnt[f];
+        uint64_t* out = arena + (size_t)gates[gi].out_slot[f] * slot_stride;
+        for (int c = tl; c <= big; c += NT) {
+            const int pp = c < big ? c / N : K, t = c < big ? c % N : 0;
+            const int j = t == 0 ? 0 : N - t;
+            const uint64_t v = w_step64<N>(accs + pp * N, tf, nt, j);
+            out[c] = t != 0 ? (uint64_t)0 - v : v;
+        }
+    }
+}
+
 // ================================================================== host side
 // compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
 // BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
@@ -1125,6 +1335,7 @@ void Device::init_fft() {
     if (const char* ev = std::getenv("FR_FFT_LANE_ELEMS")) fft_e_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_FFT_SMALL_BATCH")) fft_small_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_FFT_PAIR_BATCH")) fft_pair_ = (size_t)std::atol(ev);
+    if (const char* ev = std::getenv("FR_FFT_DUAL")) fft_dual_ = std::atoi(ev) != 0;
     if (p_.k != 1) fft_pair_ = 0;
     if (!fft_supported(p_.k, p_.N, fft_e_))
         throw Error(FR_ERR_INVALID, "device: FFT ring needs (k, N, E) in {(1, 2048, 4), (2, 1024, 4 or 8)}");
@@ -1132,7 +1343,12 @@ void Device::init_fft() {
         constexpr int N = decltype(nc)::value, K = decltype(kc)::value;
         fft_attr<N, K, 4, true>();
         fft_attr<N, K, 4, false>();
-        if constexpr (K == 1) fft_attr<N, K, 4, true, 2>();
+        if constexpr (K == 1) {
+            fft_attr<N, K, 4, true, 2>();
+            static_assert(fbr_dual_smem_bytes<N>() <= 80 * 1024, "dual shape: two workgroups per CU");
+            FFT_CHECK(hipFuncSetAttribute((const void*)k_blind_rotate_fft_dual<N>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)fbr_dual_smem_bytes<N>()));
+        }
 #ifdef FR_LAT_E2
         if constexpr (fft_shape_ok<N, K, 2>()) fft_attr<N, K, 2, true>();
 #endif
@@ -1212,7 +1428,14 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
         }
 #endif
         if (n <= fft_small_) go(I4{}, std::true_type{}, B1{});
-        else if (n <= fft_pair_) go(I4{}, std::true_type{}, std::integral_constant<int, 2>{});  // (k = 1)
+        else if (n <= fft_pair_ && K == 1 && fft_dual_) {
+            if constexpr (K == 1)
+                hipExtLaunchKernelGGL(k_blind_rotate_fft_dual<N>, dim3((unsigned)n), dim3(N / 8),
+                                      (uint32_t)fbr_dual_smem_bytes<N>(), s, (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0,
+                                      d_ks, p_.ks_stride(), p_.n, d_gates, (int)n,
+                                      (const double2*)d_fbsk_[fbsk_index(4)], (const double2*)d_ftw_,
+                                      (const double2*)d_fqt_, (const uint16_t*)d_fleaf_, d_arena_, p_.slot_stride());
+        } else if (n <= fft_pair_) go(I4{}, std::true_type{}, std::integral_constant<int, 2>{});  // (k = 1)
         else if (fft_e_ == 4) go(I4{}, std::false_type{}, B1{});
         else go(I8{}, std::false_type{}, B1{});
     });

@@ -321,3 +321,35 @@ def test_fft_pair_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, coun
     assert (got == tp.dev_blind_rotate(ks, luts)).all()
     for i in (0, 1, 3, count // 2, count - 1):
         assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("count", [257, 512])
+def test_fft_dual_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, count):
+    """The dual shape (FR_FFT_DUAL=1, k = 1: one bootstrap per 4-wave workgroup, both
+    polynomials in every lane, no MAC exchange, two workgroups per CU) bit-exact against
+    the oracle on sampled rows and against the pair shape on every row, including rows
+    with runs of zero pairs; and a whole /abc/ x 256 match bit-identical to the pair
+    shape's."""
+    if point[0] != 1:
+        pytest.skip("the dual shape is the k = 1 geometry")
+    dual = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_DUAL=1)
+    pair = _shape_ctx(key_blob, point, monkeypatch)
+    O = oracle_fft
+    rng = np.random.default_rng(count + 7)
+    ks = rng.integers(0, 2**64 - 1, (count, O.n + 1), dtype=np.uint64, endpoint=True)
+    ks[0, 0:200] = 0
+    ks[3, 1:O.n] = 0
+    luts = [[(7 * m + i) % 16 for m in range(16)] for i in range(count)]
+    got = dual.dev_blind_rotate(ks, luts)
+    assert (got == pair.dev_blind_rotate(ks, luts)).all()
+    for i in (0, 1, 3, count // 2, count - 1):
+        assert (got[i] == O.blind_rotate(ks[i], luts[i])).all(), i
+    if count == 512:
+        s = "".join(chr(c) for c in rng.integers(0x20, 0x7F, 256)).replace("abc", "abd")
+        s = s[:150] + "abc" + s[153:]
+        words = []
+        for c in (dual, pair):
+            o, _ = c.has_match(c.upload_radix(c.encrypt_str(s, seed=9)), "/abc/")
+            words.append(c.download_radix(o))
+        assert np.array_equal(words[0], words[1]) and dual.decrypt_radix(words[0]) == 1
