@@ -81,3 +81,31 @@ def test_shard_starts_partition():
                 assert 0 <= lo <= hi <= L
                 covered += list(range(lo, hi))
             assert covered == list(range(L))
+
+
+@pytest.mark.parametrize("pattern,reach", [("/abc/", 2), ("/the/i", 2), ("/a.c/", 2), ("/^ab/", 1)])
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_content_window_covers_the_starts(pattern, reach, world):
+    """fheregex.content_window (bench.py's start shards hold only this window): the
+    characters a start range's circuit reads, from the lowered schedule -- for a
+    fixed-width pattern, the starts themselves plus width - 1 characters, clipped at the
+    end of the content (engine.rs:45-214: a branch reads the characters after its start)."""
+    L = 256 * world
+    for r in range(world):
+        lo, hi = F.shard_starts(L, world, r)
+        wlo, whi = F.content_window(L, pattern, lo, hi)
+        if pattern.startswith("/^"):
+            assert (wlo, whi) == ((0, reach + 1) if r == 0 else (lo, lo))  # anchored: start 0 only
+            continue
+        assert wlo == lo and whi == min(L, hi + reach), (r, wlo, whi)
+
+
+def test_or_each_checks_group_sizes():
+    """Context.or_each (the batched final bitor of start-sharded matches) takes 1..16
+    booleans per group (one threshold gate each), refused before any device call."""
+    ctx = F.Context(-1)
+    with pytest.raises(ValueError):
+        ctx.or_each([list(range(17))])
+    with pytest.raises(ValueError):
+        ctx.or_each([[]])
+    assert ctx.or_each([]) == []
