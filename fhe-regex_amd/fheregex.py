@@ -192,7 +192,11 @@ _SIGS = {
 
 
 def lib():
-    """Load the in-tree libfheregex.so (fails loudly if it was not built)."""
+    """Load the in-tree libfheregex.so (fails loudly if it was not built).
+
+    A process that also uses torch on the GPU imports torch first: the torch wheel
+    bundles its own HIP runtime with the soname of /opt/rocm's, so loaded first it is the
+    one runtime this library binds to; loaded second, torch finds no device."""
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):

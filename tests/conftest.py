@@ -2,6 +2,10 @@ import os
 import sys
 
 import pytest
+# torch first: its wheel bundles its own HIP runtime (libamdhip64, same soname as
+# /opt/rocm's); loaded after libfheregex.so's, torch would find no device.  With torch's
+# loaded first, libfheregex.so binds to that one runtime (as in bench.py).
+import torch  # noqa: F401
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (os.path.join(REPO, "fhe-regex_amd"), os.path.join(REPO, "oracle"), os.path.join(REPO, "tests")):
