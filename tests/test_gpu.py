@@ -818,7 +818,8 @@ def test_fuzz_encrypted_vs_oracle(gctx):
 
 
 # ------------------------------------------------ whole matches, word for word
-def _match_words_vs_oracle(gctx, O, content, pattern, seed, engine=F.ENGINE_AUTO, grammar=F.GRAMMAR_REFERENCE):
+def _match_words_vs_oracle(gctx, O, content, pattern, seed, engine=F.ENGINE_AUTO, grammar=F.GRAMMAR_REFERENCE,
+                           lowering=F.LOWER_THRESHOLD, multi_value=True):
     """One has_match on the device against the oracle's evaluation of the same lowered
     schedule (fr_schedule_match: fr_job semantics, oracle_ffi.run_schedule) on the same
     content LWEs and the same server key: the result ciphertext word for word
@@ -828,7 +829,8 @@ def _match_words_vs_oracle(gctx, O, content, pattern, seed, engine=F.ENGINE_AUTO
     hs = gctx.upload_radix(ct)
     out, st = gctx.has_match(hs, pattern)
     got = gctx.download_radix(out)
-    S = F.schedule_match(len(content), pattern, engine=engine, grammar=grammar)
+    S = F.schedule_match(len(content), pattern, engine=engine, grammar=grammar, lowering=lowering,
+                         multi_value=multi_value)
     assert (len(S.jobs), len(S.level_off) - 1) == (st.blind_rotations, st.levels)
     exp = O.run_schedule(S, ct)
     assert np.array_equal(got[0], exp), (pattern, len(content))
@@ -969,3 +971,25 @@ def test_match_words_full_size_configs(gctx, oracle_k1, which):
         gctx.set_grammar(F.GRAMMAR_REFERENCE)
     exp = ro.has_match_reach(content, pat, ext=True) if which == "config3" else ro.has_match_reach(content, pat)
     assert got == exp == 1
+
+
+@pytest.mark.parametrize("variant", ["faithful", "no-multi-value"])
+def test_match_words_lowering_variants(gctx, oracle_k1, variant):
+    """The reference-structured lowering (FR_LOWER_FAITHFUL: one gate group per smart_*
+    op, execution.rs:64-195; 743 PBS for /abc/ x 64) and the threshold lowering without
+    multi-value bootstrapping, word for word against the oracle's schedule evaluation."""
+    rng = np.random.default_rng(41)
+    s = _printable(rng, 64).replace("abc", "abd")
+    s = s[:20] + "abc" + s[23:]
+    if variant == "faithful":
+        gctx.set_lowering(F.LOWER_FAITHFUL)
+    else:
+        gctx.set_multi_value(False)
+    try:
+        got = _match_words_vs_oracle(gctx, oracle_k1, s, "/abc/", 42,
+                                     lowering=F.LOWER_FAITHFUL if variant == "faithful" else F.LOWER_THRESHOLD,
+                                     multi_value=variant != "no-multi-value")
+    finally:
+        gctx.set_lowering(F.LOWER_THRESHOLD)
+        gctx.set_multi_value(True)
+    assert got == 1
