@@ -30,7 +30,8 @@ their status; under an external launcher WORLD_SIZE must equal --gpus.
     match, no data-path collective) into `weak_matches`, never `value`.
     --shard matches makes that the timed mode.
   --scaling strong: the named content length is fixed and ONE match is split
-    across the ranks (fr_shard_* C-ABI).  --shard closure (default,
+    across the ranks (fr_shard_* C-ABI; --shard starts: its start offsets, each rank
+    matching its range on its window, the same gather and OR as the weak mode).  --shard closure (default,
     fheregex.run_closure_sharded): the jobs feeding the top of the circuit are
     cut into contiguous parts, each rank runs the dependency closure of its part,
     one all_gather_into_tensor (RCCL, device to device) brings the parts' LWEs to
@@ -303,7 +304,7 @@ def resolve_mode(scaling: str, shard: str, world: int, matches: int):
     shard = shard or ("closure" if strong else "starts")
     if world == 1:
         return False, "matches"
-    if strong != (shard in ("closure", "level")):
+    if shard != "starts" and strong != (shard in ("closure", "level")):  # start shards: either scaling
         raise ValueError(f"--shard {shard} does not belong to --scaling {scaling}")
     if shard != "matches" and matches != 1:
         raise ValueError("--matches > 1 runs with --shard matches (or N = 1)")
@@ -422,7 +423,7 @@ def main():
     chars = args.chars or W["chars"]
     M = args.matches
     starts = shard == "starts"
-    L = chars * world if starts else chars
+    L = chars * world if starts and not strong else chars  # weak start shards: --chars per GPU
 
     def plant(m):
         """content of match m of this rank (weak matches: every rank its own)"""
@@ -458,7 +459,7 @@ def main():
 
     plan = None
     phase = {}
-    if strong:
+    if strong and not starts:
         gather = F.torch_all_gather()
         plan = F.ShardPlan(ctx, handles, pattern)
         sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
@@ -467,7 +468,7 @@ def main():
             runs, _, top = cparts
             closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
             closure_rot[0] += sum(b - a for rl in top for a, b in rl)
-    elif starts and world > 1:
+    if starts and world > 1:
         gather = F.torch_all_gather()
 
     def step(times=None):
@@ -848,7 +849,7 @@ def main():
         par = (f"start-offset shards x{world} (each rank its start range on its content window; {coll} "
                f"all_gather of the per-rank booleans, stream-ordered after each match; rank 0 ORs every step's "
                f"booleans in one launch at the end of the timed region)")
-    work = f"{args.workload}: {pattern} on {L} chars" + (f" ({chars} per GPU)" if starts else "")
+    work = f"{args.workload}: {pattern} on {L} chars" + (f" ({chars} per GPU)" if starts and not strong else "")
     if M > 1 or (world > 1 and shard == "matches"):
         work += f", {M} match(es) per GPU per step"
     line = {

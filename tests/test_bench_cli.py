@@ -56,6 +56,7 @@ def test_mode_defaults():
     assert bench.resolve_mode("weak", "matches", 8, 4) == (False, "matches")
     assert bench.resolve_mode("strong", "", 8, 1) == (True, "closure")
     assert bench.resolve_mode("strong", "level", 2, 1) == (True, "level")
+    assert bench.resolve_mode("strong", "starts", 4, 1) == (True, "starts")  # fixed content, starts split
     with pytest.raises(ValueError):
         bench.resolve_mode("weak", "closure", 2, 1)
     with pytest.raises(ValueError):
