@@ -835,7 +835,10 @@ k_ks_digits(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict
 // 16 KSL digits are KSL whole 16-byte pieces of the fragment-ordered digit row (k = 16 KSL q ..
 // 16 KSL q + 16 KSL - 1 starts a piece), stored as 16-byte writes, where k_ks_digits's byte
 // stores scatter every digit over 16-byte pieces of 10 fragments; the inputs load as 16-byte
-// vectors.  (needs big % 16 == 0; the body coefficient by thread 0)
+// vectors.  (needs big % 16 == 0)  The inputs' slot lookups (content map included) and their
+// body coefficients are fetched by one thread per input at once, and the mask loads of four
+// inputs are in flight together: with one input at a time, a small level's fan-in-16 gates
+// paid sixteen dependent memory round trips (≈19 µs per launch at 1-16 gates).
 template <int KSB, int KSL>
 __global__ void __launch_bounds__(128)
 k_ks_digits16(const DevGate* __restrict__ gates, int B, const uint64_t* __restrict__ arena, int slot_stride,
@@ -848,23 +851,52 @@ k_ks_digits16(const DevGate* __restrict__ gates, int B, const uint64_t* __restri
             for (int c = 0; c < KSL; ++c) *(int4*)(dig + ks_frag(g, 16 * (q * KSL + c), KT)) = int4{0, 0, 0, 0};
         return;
     }
+    __shared__ int slot_s[16];
+    __shared__ uint64_t w_s[16], body_s[16];
     const DevGate& gg = gates[g];
     const int nin = gg.n_in;
+    if (threadIdx.x < nin) {
+        const int i = threadIdx.x;
+        const int slot = arena_slot(gg.in_slot[i], cmap);
+        const uint64_t w = (uint64_t)(int64_t)gg.in_w[i];
+        slot_s[i] = slot;
+        w_s[i] = w;
+        body_s[i] = w * arena[(size_t)slot * slot_stride + big];
+    }
     for (int t = threadIdx.x; t < ks_n; t += blockDim.x) ks[(size_t)g * ks_stride + t] = 0;
+    __syncthreads();
     if (threadIdx.x == 0) {  // column n of the output row (the body); the MFMA pass subtracts
         uint64_t v = (uint64_t)(int64_t)gg.offset << (DELTA_LOG - 1);
-        for (int q = 0; q < nin; ++q)
-            v += (uint64_t)(int64_t)gg.in_w[q] * arena[(size_t)arena_slot(gg.in_slot[q], cmap) * slot_stride + big];
+        for (int q = 0; q < nin; ++q) v += body_s[q];
         ks[(size_t)g * ks_stride + ks_n] = v;
     }
     for (int q = threadIdx.x; q < groups; q += blockDim.x) {
         uint64_t v[16];
 #pragma unroll
         for (int e = 0; e < 16; ++e) v[e] = 0;
-        for (int qi = 0; qi < nin; ++qi) {
-            const uint64_t w = (uint64_t)(int64_t)gg.in_w[qi];
-            const ulonglong2* src =
-                (const ulonglong2*)(arena + (size_t)arena_slot(gg.in_slot[qi], cmap) * slot_stride + 16 * q);
+        int qi = 0;
+        for (; qi + 4 <= nin; qi += 4) {  // four inputs' loads in flight
+            ulonglong2 x[4][8];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const ulonglong2* src = (const ulonglong2*)(arena + (size_t)slot_s[qi + u] * slot_stride + 16 * q);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) x[u][e] = src[e];
+            }
+            __builtin_amdgcn_sched_barrier(0);  // keep the 32 loads ahead of their first use
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const uint64_t w = w_s[qi + u];
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                    v[2 * e] += w * x[u][e].x;
+                    v[2 * e + 1] += w * x[u][e].y;
+                }
+            }
+        }
+        for (; qi < nin; ++qi) {
+            const uint64_t w = w_s[qi];
+            const ulonglong2* src = (const ulonglong2*)(arena + (size_t)slot_s[qi] * slot_stride + 16 * q);
 #pragma unroll
             for (int e = 0; e < 8; ++e) {
                 const ulonglong2 x = src[e];
