@@ -255,16 +255,20 @@ def pmc_figures(params, path: str):
             "source": os.path.relpath(path, REPO), "stale": d.get("kernel_sha") != sha}
 
 
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
 def spawn_ranks(n: int, argv) -> int:
     """`--gpus N` without a launcher: start N rank processes of this script with
     torch.distributed.run on 127.0.0.1 (one per GPU) and return their exit status.
     The caller has touched no GPU (no HIP call, no torch.cuda query) and never
     re-execs: the ranks are children."""
-    import socket
-
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
-        sk.bind(("127.0.0.1", 0))
-        port = sk.getsockname()[1]
+    port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
@@ -297,11 +301,16 @@ def spawn_probe(world: int, rank: int):
                           "pids": [r[1] for r in rows], "parent_pids": [r[2] for r in rows]}))
 
 
-def resolve_mode(scaling: str, shard: str, world: int, matches: int):
+def resolve_mode(scaling: str, shard: str, world: int, matches: int, group1: bool = False):
     """(strong, shard) of a run: one GPU runs the plain (or batched) match; N > 1 weak
-    defaults to start-offset shards, strong to closure sharding."""
+    defaults to start-offset shards, strong to closure sharding.  group1 (--one-rank-group):
+    N = 1 runs the N > 1 start-shard pipeline over a one-rank process group."""
     strong = scaling == "strong" and world > 1
     shard = shard or ("closure" if strong else "starts")
+    if world == 1 and group1:
+        if shard != "starts" or matches != 1:
+            raise ValueError("--one-rank-group runs the start-shard pipeline (--shard starts, --matches 1)")
+        return False, "starts"
     if world == 1:
         return False, "matches"
     if shard != "starts" and strong != (shard in ("closure", "level")):  # start shards: either scaling
@@ -326,6 +335,10 @@ def main():
                          "(independent matches per rank, no data-path collective); strong: closure (default; each "
                          "rank runs the dependency closure of its part of the top's inputs, one gather to rank 0) or "
                          "level (job slices per level, all-gathered level by level)")
+    ap.add_argument("--one-rank-group", action="store_true",
+                    help="N = 1: run the N > 1 start-shard pipeline (process group, stream-ordered export, "
+                         "all_gather, OR on rank 0) with a one-rank group of --dist-backend, so the collective "
+                         "path runs on a one-GPU box")
     ap.add_argument("--spawn-probe", action="store_true",
                     help="launcher test: the ranks meet over gloo and rank 0 prints who ran (no GPU)")
     ap.add_argument("--weak-matches-steps", type=int, default=-1,
@@ -386,7 +399,7 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     try:
-        strong, shard = resolve_mode(args.scaling, args.shard, world, args.matches)
+        strong, shard = resolve_mode(args.scaling, args.shard, world, args.matches, args.one_rank_group)
     except ValueError as e:
         ap.error(str(e))
     import torch
@@ -395,9 +408,14 @@ def main():
     # one process per GPU; ranks beyond the visible devices (a gloo rehearsal on a
     # one-GPU box) share devices round-robin
     device = local_rank % max(1, torch.cuda.device_count())
-    if world > 1:
+    if world > 1 or args.one_rank_group:
         import torch.distributed as dist
 
+        if world == 1:  # a one-rank group without a launcher
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(free_port()))
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
         torch.cuda.set_device(device)
         dist.init_process_group(args.dist_backend)
     coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
@@ -468,7 +486,7 @@ def main():
             runs, _, top = cparts
             closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
             closure_rot[0] += sum(b - a for rl in top for a, b in rl)
-    if starts and world > 1:
+    if starts and dist is not None:
         gather = F.torch_all_gather()
 
     def step(times=None):
@@ -656,7 +674,7 @@ def main():
 
     weak_matches = None
     wm_steps = args.steps if args.weak_matches_steps < 0 else args.weak_matches_steps
-    if shard == "starts" and world > 1 and wm_steps > 0:
+    if shard == "starts" and dist is not None and wm_steps > 0:
         # secondary record: weak scaling by matches (every rank one full-length match of
         # the workload on its own content per step, no data-path collective)
         own = make_content(kind, chars, seed=rank)
@@ -829,13 +847,13 @@ def main():
     pmc = pmc_figures(params, args.pmc)
     phys = pmc["traffic"] / (br_avg_ms / 1e3) / 1e9 if pmc and pmc.get("traffic") and br_avg_ms > 0 else None
     cpu = None
-    if args.cpu_sample > 0 and world == 1:
+    if args.cpu_sample > 0 and world == 1 and dist is None:  # its word check reads the plain match's output
         cpu = cpu_baseline(params, content, pattern, grammar, engine, lowering, args.cpu_sample,
                            args.cpu_match_max_jobs, lwes0[0] if lwes0 else None, words0)
     ms_per_step = elapsed / args.steps * 1e3
     ring_name = "fft" if params.ring == F.RING_FFT else "rns"
     coll = "RCCL" if args.dist_backend == "nccl" else "gloo (host-staged)"
-    if world == 1:
+    if world == 1 and not starts:
         par = "single GPU" + (f", {M} matches per step in shared launches" if M > 1 else "")
     elif shard == "matches":
         par = (f"dp{world}: {M} independent match(es) per rank per step on its own content, no data-path collective "

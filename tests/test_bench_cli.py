@@ -57,6 +57,10 @@ def test_mode_defaults():
     assert bench.resolve_mode("strong", "", 8, 1) == (True, "closure")
     assert bench.resolve_mode("strong", "level", 2, 1) == (True, "level")
     assert bench.resolve_mode("strong", "starts", 4, 1) == (True, "starts")  # fixed content, starts split
+    # --one-rank-group: the start-shard pipeline over a one-rank process group
+    assert bench.resolve_mode("weak", "", 1, 1, True) == (False, "starts")
+    with pytest.raises(ValueError):
+        bench.resolve_mode("weak", "matches", 1, 1, True)
     with pytest.raises(ValueError):
         bench.resolve_mode("weak", "closure", 2, 1)
     with pytest.raises(ValueError):
