@@ -2,7 +2,8 @@
 # Round-4 closing GPU pass at HEAD: parity tests, smoke, rocprofv3 trace + PMC passes
 # (tools/profile.sh), the default bench line, batched lines, one line per BASELINE
 # workload, and the launcher-free two-rank rehearsals (gloo, ranks sharing the GPU).
-#   bash tools/final_r04.sh OUTDIR [all|a|b]   (a: tests, smoke, profile, bench line; b: the rest)
+#   bash tools/final_r04.sh OUTDIR [all|a|b|p]   (a: tests, smoke, profile, bench line; b: the rest;
+#   p: profile and bench line only)
 set -o pipefail
 cd "$(dirname "$0")/.."
 out=${1:-gpurun_out/final_r04}
@@ -10,7 +11,7 @@ mkdir -p "$out"
 export TMPDIR=/tmp
 step() { local t=$1; shift; echo "== $*" >&2; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
 part=${2:-all}
-if [ "$part" != "b" ]; then
+if [ "$part" != "b" ] && [ "$part" != "p" ]; then
   step 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > "$out/gpu_tests.log" 2>&1 || { tail -40 "$out/gpu_tests.log"; exit 1; }
   tail -1 "$out/gpu_tests.log"
   step 200 python __graft_entry__.py smoke > "$out/smoke.log" 2>&1 || { cat "$out/smoke.log"; exit 1; }
@@ -24,7 +25,7 @@ import json; d=json.load(open('$out/bench.json'))
 print('match_ms=%.3f value=%.0f fresh=%.3f frac=%.3f' % (d['match_ms'], d['value'], d['fresh_content']['fresh_content_ms'], d['roofline']['frac']))
 print('probe', {k: round(v['br_ms'],3) for k, v in d['latency_probe'].items()}, 'sat', round(d['kernel_saturated']['br_pbs_per_s']))"
 fi
-[ "$part" = "a" ] && { echo done; exit 0; }
+[ "$part" = "a" ] || [ "$part" = "p" ] && { echo done; exit 0; }
 for M in 8 16; do
   step 300 python3 bench.py --steps 5 --warmup 2 --matches $M --cpu-sample 0 --probe '' --fresh-steps 0 --saturate 0 --faithful-steps 0 > "$out/bench_m$M.json" 2> "$out/bench_m$M.err" || { tail -20 "$out/bench_m$M.err"; exit 1; }
   python3 -c "
