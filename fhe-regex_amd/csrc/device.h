@@ -200,6 +200,7 @@ class Device {
         void* ev[4];  // KS start, KS end, BR start, BR end
         size_t gates, outs;
         bool lat, pair, ks;
+        bool chain;  // BR timed from the keyswitch's end event (no start event on the BR launch)
     };
     bool latency_shape(size_t n) const;  // launch_br's shape choice for n bootstraps
     bool pair_shape(size_t n) const;     // (FFT ring, k = 1: the pair shape)
@@ -208,6 +209,7 @@ class Device {
     uint64_t* d_ks_ = nullptr;
     size_t batch_cap_ = 0;
     int profiling_ = 0;  // fr_set_profiling level
+    bool timer_chain_ = true;  // level 1: stop events only (FR_TIMER_CHAIN=0: start + stop on the BR launch)
     DeviceTimers timers_;
     void* ev_[4] = {nullptr, nullptr, nullptr, nullptr};
 };

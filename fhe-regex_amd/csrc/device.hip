@@ -1279,6 +1279,7 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
     if (const char* ev = std::getenv("FR_KS_MR4_MIN")) ks_mr4_min_ = (size_t)std::atol(ev);
     if (const char* ev = std::getenv("FR_KS_MC")) ks_mc_ = std::atoi(ev);
     if (const char* ev = std::getenv("FR_KS_SPLIT")) ks_split_ = std::atoi(ev);
+    if (const char* ev = std::getenv("FR_TIMER_CHAIN")) timer_chain_ = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("FR_KS_XCD")) ks_xcd_ = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("FR_KS_LDS")) ks_lds_ = std::atoi(ev) != 0;
     if (const char* ev = std::getenv("FR_KS_DIG16")) ks_dig16_ = std::atoi(ev) != 0;
@@ -1699,10 +1700,15 @@ void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n)
     if (profiling_)
         for (auto& e : t.ev) e = take_event();
     // keyswitch events at level 2 only: two more event-stamped launches per level cost
-    // ~30 us per /abc/ match, the blind rotation's ~0 (tools/match_probe.py)
+    // ~30 us per /abc/ match (tools/match_probe.py).  Level 1 stamps stop events only: the
+    // blind rotation runs from the keyswitch's end event to its own (the launch gap between
+    // them, ~0 without a start event, counts as rotation time).  A start event on the BR
+    // launch opened a ~6.6 us gap before it and the stop events ~4.7 us after it under the
+    // kernel trace (profiles/r04/gaps/).
+    t.chain = profiling_ == 1 && timer_chain_;
     if (profiling_ >= 2) launch_ks(d_gates, n, d_ks_, t.ev[0], t.ev[1]);
-    else launch_ks(d_gates, n, d_ks_);
-    launch_br(d_gates, d_ks_, n, t.ev[2], t.ev[3]);
+    else launch_ks(d_gates, n, d_ks_, nullptr, t.chain ? t.ev[1] : nullptr);
+    launch_br(d_gates, d_ks_, n, t.chain ? nullptr : t.ev[2], t.ev[3]);
     HIP_CHECK(hipGetLastError());
     if (profiling_) {
         t.gates = n;
@@ -1747,7 +1753,7 @@ void Device::resolve_timers() {
     for (auto& t : pending_) {
         float ks = 0, br = 0;
         if (t.ks) HIP_CHECK(hipEventElapsedTime(&ks, (hipEvent_t)t.ev[0], (hipEvent_t)t.ev[1]));
-        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[2], (hipEvent_t)t.ev[3]));
+        HIP_CHECK(hipEventElapsedTime(&br, (hipEvent_t)t.ev[t.chain ? 1 : 2], (hipEvent_t)t.ev[3]));
         timers_.ks_ms += ks;
         timers_.br_ms += br;
         timers_.br_launches += 1;
