@@ -672,9 +672,6 @@ __device__ __forceinline__ uint64_t w_step64(const uint64_t* row, const uint32_t
     return acc;
 }
 
-#ifdef FR_WG_STAMPS  // experiment: per-workgroup start / end realtime stamps and XCC of a launch
-__device__ unsigned long long g_wg_stamp[3 * 4096];
-#endif
 template <int N, int K, int E, bool LAT, int B = 1>
 __global__ void __launch_bounds__((fbr_threads<N, K, E>()), (fbr_min_waves<N, K, E, LAT>()))
 k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const DevGate* __restrict__ gates,
@@ -707,9 +704,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     uint16_t* nxt = B == 1 ? (uint16_t*)(wcnt + MAX_OUT) : abar + B * 1026;  // (latency shapes) next unskipped step
 
     const int tid = threadIdx.x;
-#ifdef FR_WG_STAMPS
-    const unsigned long long wg_t0 = __builtin_amdgcn_s_memrealtime();
-#endif
     const int P = __builtin_amdgcn_readfirstlane(tid / T), tl = tid % T;  // wave-uniform polynomial
     // bootstrap b of this workgroup: gate B blockIdx + b (an odd count's last pair repeats its
     // gate and writes it once)
@@ -1093,14 +1087,6 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             }
         }
     }
-#ifdef FR_WG_STAMPS
-    __syncthreads();
-    if (tid == 0 && blockIdx.x < 4096) {
-        g_wg_stamp[3 * blockIdx.x] = wg_t0;
-        g_wg_stamp[3 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
-        g_wg_stamp[3 * blockIdx.x + 2] = (unsigned)__builtin_amdgcn_s_getreg((20) | (0 << 6) | ((4 - 1) << 11));
-    }
-#endif
 }
 
 // Dual shape (round 4 experiment, k = 1, FR_FFT_DUAL=1): one bootstrap per workgroup on
@@ -1424,36 +1410,12 @@ void Device::launch_br_fft(const DevGate* d_gates, const uint64_t* d_ks, size_t 
             constexpr int E = decltype(ec)::value;
             constexpr bool LAT = decltype(lat)::value;
             constexpr int B = decltype(bc)::value;
-            if constexpr (fft_shape_ok<N, K, E>() && (B == 1 || K == 1)) {
+            if constexpr (fft_shape_ok<N, K, E>() && (B == 1 || K == 1))
                 hipExtLaunchKernelGGL(k_blind_rotate_fft<N, K, E, LAT, B>, dim3((unsigned)((n + B - 1) / B)),
                                       dim3(fbr_threads<N, K, E>()), (uint32_t)fbr_smem_bytes<N, K, E, LAT, B>(), s,
                                       (hipEvent_t)ev_start, (hipEvent_t)ev_stop, 0, d_ks, p_.ks_stride(), p_.n, d_gates,
                                       (int)n, (const double2*)d_fbsk_[fbsk_index(E)], (const double2*)d_ftw_,
                                       (const double2*)d_fqt_, (const uint16_t*)d_fleaf_, d_arena_, p_.slot_stride());
-#ifdef FR_WG_STAMPS
-                const int nwg = (int)((n + B - 1) / B) < 4096 ? (int)((n + B - 1) / B) : 4096;
-                std::vector<unsigned long long> st(3 * nwg);
-                FFT_CHECK(hipStreamSynchronize(s));
-                FFT_CHECK(hipMemcpyFromSymbol(st.data(), HIP_SYMBOL(g_wg_stamp), 8 * st.size()));
-                unsigned long long t0 = ~0ull;
-                for (int i = 0; i < nwg; ++i) t0 = std::min(t0, st[3 * i]);
-                double smax = 0, emin = 1e30, emax = 0, dsum = 0, dmin = 1e30, dmax = 0;
-                double xe[16] = {0}, xd[16] = {0};
-                int xc[16] = {0};
-                for (int i = 0; i < nwg; ++i) {
-                    const double a = (st[3 * i] - t0) * 0.01, e = (st[3 * i + 1] - t0) * 0.01, d = e - a;  // us (100 MHz)
-                    smax = std::max(smax, a), emin = std::min(emin, e), emax = std::max(emax, e);
-                    dsum += d, dmin = std::min(dmin, d), dmax = std::max(dmax, d);
-                    const int x = (int)(st[3 * i + 2] & 15);
-                    xe[x] += e, xd[x] += d, xc[x] += 1;
-                }
-                fprintf(stderr, "WGSTAMP n=%zu B=%d wgs=%d start_max=%.1f end_min=%.1f end_max=%.1f dur_min=%.1f mean=%.1f max=%.1f |",
-                        n, B, nwg, smax, emin, emax, dmin, dsum / nwg, dmax);
-                for (int x = 0; x < 16; ++x)
-                    if (xc[x]) fprintf(stderr, " x%d:%d end%.0f dur%.0f", x, xc[x], xe[x] / xc[x], xd[x] / xc[x]);
-                fprintf(stderr, "\n");
-#endif
-            }
         };
         using I4 = std::integral_constant<int, 4>;
         using I8 = std::integral_constant<int, 8>;
