@@ -65,3 +65,20 @@ def test_mode_defaults():
         bench.resolve_mode("weak", "closure", 2, 1)
     with pytest.raises(ValueError):
         bench.resolve_mode("weak", "starts", 2, 4)
+
+
+@pytest.mark.gpu
+def test_one_rank_rccl_group_pipeline():
+    """The N > 1 start-shard pipeline over a one-rank RCCL group on the GPU (bench.py
+    --one-rank-group): process group, stream-ordered export, device all_gather, the OR on
+    rank 0 and the all-reduces run, and every step's OR decrypts to the expected bit."""
+    res = subprocess.run([sys.executable, BENCH, "--one-rank-group", "--steps", "3", "--warmup", "1", "--cpu-sample", "0",
+                          "--inflight", "0", "--faithful-steps", "0", "--fresh-steps", "0", "--probe=", "--saturate", "0",
+                          "--weak-matches-steps", "2"], capture_output=True, text=True, timeout=300, env=_env())
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 1 and d["config"]["shard"] == "starts" and "RCCL" in d["config"]["parallelism"]
+    assert d["results_ok_steps"] is True and d["result_decrypted"] == d["result_expected"] == [1]
+    assert len(d["per_rank"]) == 1 and d["weak_matches"]["results_ok_ranks"] == 1
