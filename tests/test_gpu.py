@@ -867,6 +867,51 @@ def test_match_words_fuzz_scale(gctx, oracle_k1, case):
     assert _match_words_vs_oracle(gctx, oracle_k1, cse["content"], cse["pattern"], 3000 + case) == cse["expected"]
 
 
+@pytest.mark.parametrize("world", [2, 3])
+def test_match_words_start_shards(gctx, oracle_k1, world):
+    """north_star's start-offset shards word for word: each rank's fr_has_match_range over
+    its start range on its content window against the oracle's evaluation of the same
+    ranged schedule (fr_schedule_match with start_lo / start_hi) on the same LWEs, and the
+    final bitor (Context.or_each: one sign gate over the ranks' booleans) against the
+    oracle's gate.  /the/i on 192 letters with "ThE" planted across the first shard
+    boundary (engine.rs:15-35)."""
+    L, pat = 192, "/the/i"
+    rng = np.random.default_rng(53 + world)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
+    s = bytearray(rng.choice(alpha, L))
+    for i in range(L - 2):
+        if bytes(s[i:i + 3]).lower() == b"the":
+            s[i + 2] = ord("x")
+    cut = F.shard_starts(L, world, 1)[0]
+    s[cut - 1:cut + 2] = b"ThE"
+    s = bytes(s)
+    O = oracle_k1
+    words, parts, held = [], [], []
+    for r in range(world):
+        lo, hi = F.shard_starts(L, world, r)
+        wlo, whi = F.content_window(L, pat, lo, hi)
+        win = gctx.encrypt_str(s[wlo:whi], seed=70 + r)  # [whi - wlo, 4, lwe]
+        full = np.zeros((L, 4, gctx.lwe_len), dtype=np.uint64)
+        full[wlo:whi] = win
+        hs = [F.NULL_CT] * L
+        hs[wlo:whi] = gctx.upload_radix(win)
+        out, st = gctx.has_match(hs, pat, lo, hi)
+        got = gctx.download_radix(out)
+        S = F.schedule_match(L, pat, lo, hi)
+        assert (len(S.jobs), len(S.level_off) - 1) == (st.blind_rotations, st.levels)
+        exp = O.run_schedule(S, full)
+        assert np.array_equal(got[0], exp), r
+        words.append(exp)
+        parts.append(out)
+        held += hs[wlo:whi]
+    res = gctx.or_each([parts])[0]
+    exp_or = O.gates([([(q, 1) for q in range(world)], -1, [0] * 16, 2)], np.stack(words))[0]
+    assert np.array_equal(gctx.download_radix(res)[0], exp_or)
+    assert O.decode16(exp_or)[0] == 1 == ro.has_match_reach(s.decode(), pat)
+    for h in held + parts + [res]:
+        gctx.release(h)
+
+
 # ------------------------------------- start-offset shards across contexts
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("where", ["boundary", "absent"])
