@@ -353,11 +353,13 @@ int fr_set_lowering(fr_ctx* ctx, int32_t mode);
 /* Multi-value bootstrapping: gates of one level that read the same linear
  * combination share one blind rotation (default on). */
 int fr_set_multi_value(fr_ctx* ctx, int32_t on);
-/* Device profiling: 0 off; 1 blind-rotation timers (HIP events stamped by each blind
- * rotation launch itself, hipExtLaunchKernel: no marker packets, no syncs; what bench.py's
- * timed region uses); 2 also the keyswitch timers (two more stamped launches per level,
- * ~30 us per /abc/ x 256 match).  Timers resolve at the next synchronisation.  Any
- * nonzero value other than 2 is level 1. */
+/* Device profiling: 0 off; 1 blind-rotation timers (HIP stop events stamped by the
+ * launches themselves, hipExtLaunchKernel: no marker packets, no syncs; a level's blind
+ * rotation runs from its keyswitch's stop event to its own, the launch gap between them
+ * included; what bench.py's timed region uses; FR_TIMER_CHAIN=0 stamps a start event on
+ * the blind rotation instead, 9-15 us more per launch); 2 also the keyswitch timers (start
+ * and stop events on every level's keyswitch, ~30 us per /abc/ x 256 match).  Timers
+ * resolve at the next synchronisation.  Any nonzero value other than 2 is level 1. */
 int fr_set_profiling(fr_ctx* ctx, int32_t on);
 
 /* ----- single-stage device entry points (parity tests of each kernel) ----- */
