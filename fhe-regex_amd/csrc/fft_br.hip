@@ -161,13 +161,17 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_PAIR_LOAD
 #define FR_PAIR_LOAD 2
 #endif
-// pair shape A/B knobs: key groups loaded a step ahead (2; with 1 the third group loads after
-// forward phase FR_PAIR_LOAD2), and the inverse's c ca recomputed per phase (1) or kept (0)
+// pair shape A/B knobs: key groups loaded a step ahead (FR_PAIR_PF; with 1 the third group
+// loads after forward phase FR_PAIR_LOAD2), and the inverse's c ca recomputed per phase (1) or
+// kept (0).  Round 4 (profiles/r04/ab_key_placement{,2,3}.log, 512 / 2048 bootstraps): one group
+// ahead, the second after forward phase 2 and the third after phase 4 (in the MAC barrier's
+// shadow, its registers free across the transform) 2.66-2.67 / 9.48-9.51 ms, against 2.72-2.75 /
+// 9.81-9.83 for two groups ahead and the third after phase 2; the third after phase 3: 9.65-9.67
 #ifndef FR_PAIR_PF
-#define FR_PAIR_PF 2
+#define FR_PAIR_PF 1
 #endif
 #ifndef FR_PAIR_LOAD2
-#define FR_PAIR_LOAD2 3
+#define FR_PAIR_LOAD2 4
 #endif
 #ifndef FR_PAIR_CC
 #define FR_PAIR_CC 1
@@ -845,8 +849,9 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         // phases FR_LAT_LOAD1 / FR_LAT_LOAD2 (3: none).  k = 1, NPF = 2: the third group at the
         // top (tools/ab_libs.sh: 1.34 ms; after forward phase 0 / 2 / 3: 1.33 / 1.38 / 1.38 ms;
         // after the previous inverse: 1.35 ms); k = 2 keeps it after phase 3 (1.67 vs 1.71 ms)
-        // The pair shape loads its third group after forward phase FR_PAIR_LOAD (the pair's
-        // 64 live transform values leave no room for it across the whole transform).
+        // The pair shape (NPF = 1) loads its second group after forward phase FR_PAIR_LOAD and
+        // its third after FR_PAIR_LOAD2 = 4, right before the MAC barrier (the pair's 64 live
+        // transform values leave no room for a group across the whole transform).
         constexpr int G_TOP = !LAT || B > 1 ? 3 : (NPF < 2 || K == 1) ? NPF : 3;
         constexpr int G_L1 = !LAT ? 3 : B > 1 ? NPF : G_TOP + 1 < 3 ? G_TOP + 1 : 3;
         constexpr int G_L2 = !LAT ? 3 : B > 1 ? (NPF + 1 < 3 ? NPF + 1 : 3) : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
