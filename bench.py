@@ -255,6 +255,24 @@ def pmc_figures(params, path: str):
             "source": os.path.relpath(path, REPO), "stale": d.get("kernel_sha") != sha}
 
 
+def north_star_hbm(per_shape):
+    """north_star's ">= 50% HBM roofline on the external-product kernel", evaluated at the
+    dominant launch shape (the most BR time in the timed region): the physical fraction
+    (PMC bytes per launch / launch time) decides it; the algorithmic one (48.6 MB of GGSW per
+    bootstrap) is a normalisation that counts the L2-shared key once per bootstrap"""
+    live = {k: v for k, v in per_shape.items() if v}
+    if not live:
+        return None
+    name, sh = max(live.items(), key=lambda kv: kv[1]["avg_ms"] * kv[1]["launches"])
+    phys = sh.get("hbm_physical_frac")
+    return {"target": 0.5, "shape": name, "physical_frac": phys, "algorithmic_frac": sh["hbm_algorithmic_frac"],
+            "met": bool(phys is not None and phys >= 0.5),
+            "bound": "valu/LDS exchanges (f64 FFT butterflies and the transforms' LDS exchanges and barriers; the "
+                     "key stream is shared through each XCD's L2, so HBM is not the bound)",
+            "note": "target not met and not the bound: physical HBM traffic is a few percent of 8 TB/s; the "
+                    "algorithmic figure is not a physical rate (it exceeds 1.0 at >= 512 bootstraps per launch)"}
+
+
 def free_port() -> int:
     import socket
 
@@ -263,22 +281,58 @@ def free_port() -> int:
         return sk.getsockname()[1]
 
 
-def spawn_ranks(n: int, argv) -> int:
+def spawn_ranks(n: int, argv, job_timeout: float = 0.0, script: str = "") -> int:
     """`--gpus N` without a launcher: start N rank processes of this script with
     torch.distributed.run on 127.0.0.1 (one per GPU) and return their exit status.
     The caller has touched no GPU (no HIP call, no torch.cuda query) and never
-    re-execs: the ranks are children."""
+    re-execs: the ranks are children.  job_timeout > 0: after that many seconds the
+    launcher's whole process group is killed and 124 returned (a stuck rank or
+    collective ends the job with a message instead of holding the node)."""
+    import signal
+    import threading
+
     port = free_port()
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+           "--master-addr", "127.0.0.1", "--master-port", str(port), script or os.path.abspath(__file__)] + list(argv)
     env = dict(os.environ)
     env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver (RCCL)
     # the ranks' stdout: the JSON line passes, anything else (launcher / gloo chatter) goes to stderr
-    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1, start_new_session=True)
+    expired = threading.Event()
+
+    def kill_job():
+        """the launcher and every process under it (torch.distributed.run starts each rank
+        in a process group of its own, so the launcher's group alone misses them)"""
+        expired.set()
+        print(f"bench.py: the {n} ranks did not finish within --job-timeout {job_timeout:.0f} s; "
+              f"killing the launcher and its ranks", file=sys.stderr, flush=True)
+        try:
+            import psutil
+
+            tree = psutil.Process(proc.pid).children(recursive=True)
+        except Exception:  # psutil absent or the launcher gone: its own group below
+            tree = []
+        for p in tree:
+            try:
+                p.kill()
+            except Exception:
+                pass
+        try:
+            os.killpg(proc.pid, signal.SIGKILL)
+        except ProcessLookupError:
+            pass
+
+    timer = threading.Timer(job_timeout, kill_job) if job_timeout > 0 else None
+    if timer is not None:
+        timer.daemon = True
+        timer.start()
     for line in proc.stdout:
         (sys.stdout if line.lstrip().startswith("{") else sys.stderr).write(line)
         sys.stdout.flush()
-    return proc.wait()
+    rc = proc.wait()
+    if timer is not None:
+        timer.cancel()
+    return 124 if expired.is_set() else rc
 
 
 def spawn_probe(world: int, rank: int):
@@ -301,10 +355,39 @@ def spawn_probe(world: int, rank: int):
                           "pids": [r[1] for r in rows], "parent_pids": [r[2] for r in rows]}))
 
 
+# N > 1 default (scaling, shard) per workload: the metric (and config 2) grows the content
+# with N, split by start offsets (weak); config 4 is BASELINE's "1024-char content, start
+# offsets sharded across 8 GPUs", so its value is the named length split by start offsets
+# (strong); the anchored configs 3 and 5 have one start, so one match is split by its
+# dependency closures (strong)
+N_GT_1_DEFAULT = {"metric": ("weak", "starts"), "config2": ("weak", "starts"), "config3": ("strong", "closure"),
+                  "config4": ("strong", "starts"), "config5": ("strong", "closure")}
+
+
+def default_mode(workload: str, scaling: str, shard: str):
+    """--scaling / --shard as given, or the workload's N > 1 default where left empty"""
+    ds, dsh = N_GT_1_DEFAULT[workload]
+    if not scaling:
+        scaling = ds
+        if not shard and scaling == ds:
+            shard = dsh
+    return scaling, shard
+
+
+def nccl_device_guard(backend: str, local_world: int, n_devices: int):
+    """RCCL (like NCCL) refuses two ranks on one device: under nccl every local rank
+    needs its own GPU.  Returns an error message, or None."""
+    if backend == "nccl" and local_world > n_devices:
+        return (f"--dist-backend nccl needs one GPU per rank: {local_world} local rank(s) but "
+                f"{n_devices} visible device(s) (use --dist-backend gloo to rehearse ranks sharing a GPU)")
+    return None
+
+
 def resolve_mode(scaling: str, shard: str, world: int, matches: int, group1: bool = False):
     """(strong, shard) of a run: one GPU runs the plain (or batched) match; N > 1 weak
     defaults to start-offset shards, strong to closure sharding.  group1 (--one-rank-group):
     N = 1 runs the N > 1 start-shard pipeline over a one-rank process group."""
+    scaling = scaling or "weak"
     strong = scaling == "strong" and world > 1
     shard = shard or ("closure" if strong else "starts")
     if world == 1 and group1:
@@ -327,9 +410,10 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="metric", choices=sorted(WORKLOADS))
-    ap.add_argument("--scaling", default="weak", choices=["strong", "weak"],
-                    help="N>1: weak = per-GPU work fixed (default); strong = the workload's content split across "
-                         "ranks (one match)")
+    ap.add_argument("--scaling", default="", choices=["", "strong", "weak"],
+                    help="N>1: weak = per-GPU work fixed; strong = the workload's content split across ranks (one "
+                         "match); default per workload (N_GT_1_DEFAULT: metric/config2 weak start shards, config4 "
+                         "strong start shards on its 1,024 chars, config3/config5 strong closure shards)")
     ap.add_argument("--shard", default="", choices=["", "matches", "starts", "closure", "level"],
                     help="weak: starts (default; start-offset shards + RCCL all_gather + OR on rank 0) or matches "
                          "(independent matches per rank, no data-path collective); strong: closure (default; each "
@@ -356,7 +440,7 @@ def main():
     ap.add_argument("--params", default="k1n2048", choices=["k1n2048", "k2n1024"])
     ap.add_argument("--ring", default="auto", choices=["auto", "fft", "rns"])
     ap.add_argument("--engine", default="auto", choices=["auto", "enumerate", "merged"])
-    ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful"])
+    ap.add_argument("--lowering", default="threshold", choices=["threshold", "faithful", "faithful_tree"])
     ap.add_argument("--cpu-sample", type=int, default=2048,
                     help="gates in the CPU baseline sample (0: skip; 2048 ~ 10 s on 16 threads)")
     ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
@@ -365,8 +449,20 @@ def main():
                     help="N=1: matches on newly encrypted content (encryption outside the timing; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N>1 collectives (nccl = RCCL over xGMI; gloo only to rehearse ranks sharing one GPU)")
+    ap.add_argument("--dist-timeout", type=float, default=300.0,
+                    help="seconds a rendezvous or collective may wait before the rank aborts with an error "
+                         "(init_process_group timeout; RCCL async error handling tears the rank down)")
+    ap.add_argument("--job-timeout", type=float, default=1500.0,
+                    help="--gpus N without a launcher: seconds before the spawned ranks are killed (0: none)")
+    ap.add_argument("--strong-starts-steps", type=int, default=-1,
+                    help="N>1: steps of the secondary `strong_starts` record (the workload's named length split by "
+                         "start offsets; -1: --steps; 0: skip)")
+    ap.add_argument("--faithful-tree-steps", type=int, default=3,
+                    help="N=1 metric: timed matches of the reference op mix with its AND/OR chains rebalanced "
+                         "(FR_LOWER_FAITHFUL_TREE) for the `faithful_tree` sub-record (0: skip)")
     ap.add_argument("--probe", default="1,16,254",
                     help="comma-separated batch sizes: blind-rotation ms per launch vs batch ('' to skip)")
+    ap.add_argument("--out", default="", help="also write the JSON line to this file (rank 0)")
     ap.add_argument("--pmc", default="",
                     help="PMC summary of the BR kernel (tools/pmc_summary.py); default: the newest profiles/r0N/"
                          "pmc_summary.json at k1n2048, pmc_summary_k2n1024.json at k2n1024")
@@ -375,7 +471,7 @@ def main():
         ap.error("--gpus must be >= 1")
     env_world = os.environ.get("WORLD_SIZE")
     if env_world is None and args.gpus > 1:
-        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:], args.job_timeout))
     if env_world is not None and int(env_world) != args.gpus:
         ap.error(f"--gpus {args.gpus} disagrees with WORLD_SIZE={env_world} from the launcher")
     if args.spawn_probe:
@@ -393,11 +489,15 @@ def main():
     kind = args.content or W["content"]
     grammar = W.get("grammar", F.GRAMMAR_REFERENCE)
     engine = {"auto": F.ENGINE_AUTO, "enumerate": F.ENGINE_ENUMERATE, "merged": F.ENGINE_MERGED}[args.engine]
-    lowering = F.LOWER_THRESHOLD if args.lowering == "threshold" else F.LOWER_FAITHFUL
+    lowering = {"threshold": F.LOWER_THRESHOLD, "faithful": F.LOWER_FAITHFUL,
+                "faithful_tree": F.LOWER_FAITHFUL_TREE}[args.lowering]
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    if world > 1:
+        args.scaling, args.shard = default_mode(args.workload, args.scaling, args.shard)
     try:
         strong, shard = resolve_mode(args.scaling, args.shard, world, args.matches, args.one_rank_group)
     except ValueError as e:
@@ -405,10 +505,17 @@ def main():
     import torch
 
     dist = None
-    # one process per GPU; ranks beyond the visible devices (a gloo rehearsal on a
-    # one-GPU box) share devices round-robin
+    if world > 1 or args.one_rank_group:
+        # counting devices does not initialise the GPU on this image
+        msg = nccl_device_guard(args.dist_backend, local_world, torch.cuda.device_count())
+        if msg:
+            ap.error(msg)
+    # one process per GPU; only a gloo rehearsal (ranks beyond the visible devices on a
+    # one-GPU box) shares devices round-robin
     device = local_rank % max(1, torch.cuda.device_count())
     if world > 1 or args.one_rank_group:
+        import datetime
+
         import torch.distributed as dist
 
         if world == 1:  # a one-rank group without a launcher
@@ -416,8 +523,10 @@ def main():
             os.environ.setdefault("MASTER_PORT", str(free_port()))
             os.environ.setdefault("RANK", "0")
             os.environ.setdefault("WORLD_SIZE", "1")
+        # a collective stuck past --dist-timeout aborts the rank (RCCL watchdog) instead of hanging the node
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         torch.cuda.set_device(device)
-        dist.init_process_group(args.dist_backend)
+        dist.init_process_group(args.dist_backend, timeout=datetime.timedelta(seconds=args.dist_timeout))
     coll_dev = torch.device("cuda", device) if args.dist_backend == "nccl" else torch.device("cpu")
 
     def barrier():
@@ -477,8 +586,8 @@ def main():
 
     plan = None
     phase = {}
+    gather = F.torch_all_gather() if dist is not None else None
     if strong and not starts:
-        gather = F.torch_all_gather()
         plan = F.ShardPlan(ctx, handles, pattern)
         sched = F.schedule_match(L, pattern, lowering=lowering, engine=engine, grammar=grammar)
         if shard == "closure":
@@ -486,8 +595,6 @@ def main():
             runs, _, top = cparts
             closure_rot = [sum(b - a for rl in runs[r] for a, b in rl) for r in range(world)]
             closure_rot[0] += sum(b - a for rl in top for a, b in rl)
-    if starts and dist is not None:
-        gather = F.torch_all_gather()
 
     def step(times=None):
         """one step; returns ([result handles] on rank 0 (else []), rotations run by this rank, stats)"""
@@ -519,23 +626,47 @@ def main():
         raise AssertionError("start shards run starts_pipeline")
 
     rccl = args.dist_backend == "nccl"
-    lib_stream = torch.cuda.ExternalStream(ctx.stream_ptr(), device=torch.device("cuda", device)) if starts else None
+    coll_name = "RCCL" if rccl else "gloo (host-staged)"
+    lib_stream = (torch.cuda.ExternalStream(ctx.stream_ptr(), device=torch.device("cuda", device))
+                  if starts or dist is not None else None)
 
-    def starts_pipeline(n, times=None):
+    def starts_job(Lj, seed):
+        """this rank's part of a start-sharded match over Lj chars of the workload's content:
+        its start range, the content window those starts read (encrypted into this rank's
+        arena, nothing else), the expected bit"""
+        cj = make_content(kind, Lj, seed=0)
+        jlo, jhi = F.shard_starts(Lj, world, rank)
+        jwlo, jwhi = F.content_window(Lj, pattern, jlo, jhi, lowering=lowering, engine=engine, grammar=grammar)
+        hs = [F.NULL_CT] * Lj
+        if jwhi > jwlo:
+            msgs = [(ch >> (2 * b)) & 3 for ch in cj[jwlo:jwhi] for b in range(4)]
+            blocks = ctx.encrypt_blocks(msgs, seed=seed, first_block=4 * jwlo).reshape(jwhi - jwlo, 4, ctx.lwe_len)
+            for i, h in enumerate(ctx.upload_radix(blocks)):
+                hs[jwlo + i] = h
+        exp = F.plain_match(cj, pattern, engine=engine, grammar=grammar, lowering=lowering).result_lowered
+        return {"handles": np.asarray(hs, dtype=np.uint32), "lo": jlo, "hi": jhi, "L": Lj, "expected": exp,
+                "window": (jwlo, jwhi)}
+
+    def starts_pipeline(n, times=None, job=None):
         """n start-sharded matches (north_star's per-start-offset variants + final bitor,
         engine.rs:15-35): per step every rank enqueues its start range's match, exports its
         boolean device to device into that step's row (stream-ordered) and all-gathers the
         row (RCCL on torch's stream, ordered after the export by an event on the library's
         stream; the host never waits between matches).  Rank 0 then ORs every step's
         gathered booleans in ONE launch (n independent threshold ORs).  gloo (a rehearsal:
-        ranks sharing one GPU) stages the gather through the host.  Returns ([result per
-        step] on rank 0, rotations this rank ran, last stats)."""
-        send = torch.zeros((n, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
-        recv = torch.zeros((n, world, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        ranks sharing one GPU) stages the gather through the host.  job: starts_job(...)
+        (default: the timed workload's).  Returns ([result per step] on rank 0, rotations
+        this rank ran, last stats)."""
+        jh, jlo, jhi = (handles_np, lo, hi) if job is None else (job["handles"], job["lo"], job["hi"])
+        # every row is overwritten by an export on the library's stream, which must not
+        # overtake the allocation's work on torch's stream (ADVICE r04)
+        send = torch.empty((n, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        recv = torch.empty((n, world, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        lib_stream.wait_stream(torch.cuda.current_stream())
         rot, st = 0, None
         for i in range(n):
             t = time.perf_counter()
-            out, st = ctx.has_match(handles_np, pattern, lo, hi)
+            out, st = ctx.has_match(jh, pattern, jlo, jhi)
             rot += st.blind_rotations
             if rccl:
                 ctx.export_bool_device_async([out], send[i].data_ptr())
@@ -705,8 +836,55 @@ def main():
         for h in own_hs:
             ctx.release(int(h))
 
+    strong_starts = None
+    ss_steps = args.steps if args.strong_starts_steps < 0 else args.strong_starts_steps
+    if starts and strong and dist is not None:
+        strong_starts = {"same_as_value": True,
+                         "note": "the timed region is already the named length split by start offsets"}
+    elif dist is not None and ss_steps > 0:
+        # secondary record: the workload's NAMED length (256 chars for the metric, 1,024 for
+        # config 4, ...) split by start offsets across the ranks -- north_star's split at
+        # BASELINE's length, strong scaling -- beside a value on other terms; never `value`
+        job = starts_job(chars, 7 + 1000 * rank + 77)
+        for h in starts_pipeline(1, job=job)[0]:  # warm-up (plan)
+            ctx.release(h)
+        sphase = {}
+        barrier()
+        t = time.perf_counter()
+        s_outs, s_rot, _ = starts_pipeline(ss_steps, sphase, job=job)
+        barrier()
+        sel = time.perf_counter() - t
+        s_ok = all(ctx.decrypt_radix(ctx.download_radix(o)) == job["expected"] for o in s_outs) if rank == 0 else True
+        for o in s_outs:
+            ctx.release(o)
+        tt = torch.tensor([sel, float(s_rot), float(s_ok)], dtype=torch.float64, device=coll_dev)
+        mx, sm = tt[:1].clone(), tt[1:].clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        skeys = ["starts_ms", "gather_ms", "or_ms"]
+        mine = torch.tensor([sphase.get(kk, 0.0) / ss_steps for kk in skeys] + [float(s_rot) / ss_steps, sel * 1e3 / ss_steps],
+                            dtype=torch.float64, device=coll_dev)
+        allr = [torch.zeros_like(mine) for _ in range(world)]
+        dist.all_gather(allr, mine)
+        s_per_rank = []
+        for r, v in enumerate(allr):
+            v = v.cpu().tolist()
+            d = {"rank": r, "rotations_run": v[len(skeys)], "step_ms": v[len(skeys) + 1]}
+            d.update({kk: round(x, 4) for kk, x in zip(skeys, v) if x})
+            s_per_rank.append(d)
+        strong_starts = {"value": float(sm[0]) / float(mx[0]), "unit": "gate-bootstraps/s",
+                         "ms_per_step": float(mx[0]) * 1e3 / ss_steps, "steps": ss_steps,
+                         "content_chars": job["L"], "scaling": "strong",
+                         "workload": f"{pattern} on {job['L']} chars (the workload's named length) split by start "
+                                     f"offsets over {world} ranks, {coll_name} gather, OR on rank 0",
+                         "results_ok_steps": bool(sm[1] >= world), "result_expected": job["expected"],
+                         "per_rank": s_per_rank, "note": "secondary: never `value`"}
+        for h in job["handles"]:
+            if h != F.NULL_CT:
+                ctx.release(int(h))
+
     inflight = None
-    if args.inflight > 1 and world == 1 and M == 1 and rank == 0:
+    if args.inflight > 1 and world == 1 and M == 1 and rank == 0 and not starts:
         # serving view: C independent single matches in flight, one per context (each context
         # its own stream, arena and copy of the keys), dealt round-robin; each match is the
         # full workload match, bit-identical to the timed region's
@@ -759,31 +937,43 @@ def main():
                         "what": "one start-sharded match end to end (rank 0's view after barriers): the ranks' "
                                 "matches, the boolean all-gather and the OR on rank 0"}
 
-    faithful = None
-    if args.faithful_steps > 0 and world == 1 and M == 1 and rank == 0 and lowering == F.LOWER_THRESHOLD:
-        # the reference-structured lowering (one gate group per smart_* op, execution.rs:64-195)
-        # on the same content: its PBS count and levels are the reference's op structure
-        ctx.set_lowering(F.LOWER_FAITHFUL)
+    def lowering_record(mode, steps, label):
+        """the same content's match under another lowering (one gate group per smart_* op,
+        execution.rs:64-195): its PBS count and levels are the reference's op structure"""
+        ctx.set_lowering(mode)
         t = time.perf_counter()
         o, stf = ctx.has_match(handles_np, pattern)
         torch.cuda.synchronize()
         cold_ms = (time.perf_counter() - t) * 1e3
         ctx.release(o)
         t = time.perf_counter()
-        for i in range(args.faithful_steps):
+        for i in range(steps):
             o, stf = ctx.has_match(handles_np, pattern)
-            if i + 1 < args.faithful_steps:
+            if i + 1 < steps:
                 ctx.release(o)
         torch.cuda.synchronize()
-        fms = (time.perf_counter() - t) * 1e3 / args.faithful_steps
+        fms = (time.perf_counter() - t) * 1e3 / steps
         fres = ctx.decrypt_radix(ctx.download_radix(o))
         ctx.release(o)
         ctx.set_lowering(lowering)
-        faithful = {"lowering": "faithful (FR_LOWER_FAITHFUL: eq/gt/le = 3 PBS, and/or = 1, not linear)",
-                    "match_ms": fms, "first_call_ms": cold_ms, "steps": args.faithful_steps,
-                    "pbs": int(stf.pbs), "blind_rotations": int(stf.blind_rotations), "levels": int(stf.levels),
-                    "pbs_per_s": stf.pbs / (fms / 1e3), "result_decrypted": fres,
-                    "vs_threshold_ms": ms_per_step_local}
+        return {"lowering": label, "match_ms": fms, "first_call_ms": cold_ms, "steps": steps,
+                "pbs": int(stf.pbs), "blind_rotations": int(stf.blind_rotations), "levels": int(stf.levels),
+                "pbs_per_s": stf.pbs / (fms / 1e3), "result_decrypted": fres, "result_expected": expected[0],
+                "vs_threshold_ms": ms_per_step_local}
+
+    faithful = faithful_tree = None
+    if world == 1 and M == 1 and rank == 0 and lowering == F.LOWER_THRESHOLD and not starts:
+        if args.faithful_steps > 0:
+            faithful = lowering_record(F.LOWER_FAITHFUL, args.faithful_steps,
+                                       "faithful (FR_LOWER_FAITHFUL: eq/gt/le = 3 PBS, and/or = 1, not linear; the "
+                                       "reference's serial fold, engine.rs:22-35)")
+        if args.faithful_tree_steps > 0:
+            # the reference's op mix (the same gates as `faithful`) with its AND/OR chains
+            # rebalanced into binary trees of least depth (SURVEY §7 step 5): log depth
+            faithful_tree = lowering_record(F.LOWER_FAITHFUL_TREE, args.faithful_tree_steps,
+                                            "faithful_tree (FR_LOWER_FAITHFUL_TREE: the faithful gates, eq/gt/le = 3 "
+                                            "PBS, and/or = 1, with every unshared AND/OR chain rebalanced; never "
+                                            "`value`)")
 
     kernel = None
     if args.saturate and rank == 0:
@@ -841,10 +1031,17 @@ def main():
                 "hbm_physical_bytes_per_launch": phys_b, "hbm_physical_GBps": phys,
                 "hbm_physical_frac": phys / HBM_PEAK_GBS if phys is not None else None}
 
+    pmc = pmc_figures(params, args.pmc)
+    per_shape = {
+        "latency": shape_line("latency", lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
+        "pair": shape_line("pair", lat["pair_br_ms"], lat["pair_launches"], lat["pair_gates"], 2),
+        "throughput": shape_line("throughput", br_ms - lat["lat_br_ms"] - lat["pair_br_ms"],
+                                 br_launches - lat["lat_launches"] - lat["pair_launches"],
+                                 br_gates - lat["lat_gates"] - lat["pair_gates"]),
+    }
     achieved_tf = br_gates * fpp / (br_ms / 1e3) / 1e12 if br_ms > 0 else 0.0
     alg_gbs = (br_gates * bpp) / (br_ms / 1e3) / 1e9 if br_ms > 0 else 0.0
     br_avg_ms = br_ms / max(br_launches, 1)
-    pmc = pmc_figures(params, args.pmc)
     phys = pmc["traffic"] / (br_avg_ms / 1e3) / 1e9 if pmc and pmc.get("traffic") and br_avg_ms > 0 else None
     cpu = None
     if args.cpu_sample > 0 and world == 1 and dist is None:  # its word check reads the plain match's output
@@ -916,13 +1113,7 @@ def main():
             "br_launches": br_launches,
             "br_avg_ms": br_avg_ms,
             "br_gates_per_launch": br_gates / max(br_launches, 1),
-            "per_shape": {
-                "latency": shape_line("latency", lat["lat_br_ms"], lat["lat_launches"], lat["lat_gates"]),
-                "pair": shape_line("pair", lat["pair_br_ms"], lat["pair_launches"], lat["pair_gates"], 2),
-                "throughput": shape_line("throughput", br_ms - lat["lat_br_ms"] - lat["pair_br_ms"],
-                                         br_launches - lat["lat_launches"] - lat["pair_launches"],
-                                         br_gates - lat["lat_gates"] - lat["pair_gates"]),
-            },
+            "per_shape": per_shape,
             "valu_issue": None if not pmc or pmc.get("valu_per_cu_clk") is None else {
                 "achieved": pmc["valu_per_cu_clk"],
                 "unit": "VALU wave64 instructions per active-CU clock (SQ_INSTS_VALU, rocprofv3 PMC)",
@@ -940,6 +1131,7 @@ def main():
                                   "normalisation, not a physical rate -- bootstraps in flight share each step's key "
                                   "through the XCD's L2, so at >= 512 bootstraps per launch it exceeds the 8 TB/s peak",
             },
+            "north_star_hbm": north_star_hbm(per_shape),
             "pmc_source": pmc["source"] if pmc else None,
             "pmc_stale": pmc["stale"] if pmc else None,
         },
@@ -948,11 +1140,16 @@ def main():
         "inflight": inflight,
         "weak_matches": weak_matches,
         "faithful": faithful,
+        "faithful_tree": faithful_tree,
+        "strong_starts": strong_starts,
         "kernel_saturated": kernel,
         "latency_probe": probe,
         "cpu_baseline": cpu,
     }
-    print(json.dumps(line))
+    print(json.dumps(line), flush=True)
+    if args.out:
+        with open(args.out, "w") as f:
+            f.write(json.dumps(line) + "\n")
     if plan is not None:
         plan.free()
     if dist is not None:

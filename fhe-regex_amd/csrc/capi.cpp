@@ -732,7 +732,7 @@ int fr_ctx_destroy(fr_ctx* ctx) {
 
 int fr_set_lowering(fr_ctx* ctx, int32_t mode) {
     FR_TRY({
-        NEED(ctx && (mode == FR_LOWER_FAITHFUL || mode == FR_LOWER_THRESHOLD));
+        NEED(ctx && (mode == FR_LOWER_FAITHFUL || mode == FR_LOWER_THRESHOLD || mode == FR_LOWER_FAITHFUL_TREE));
         ctx->lowering = mode;
     })
 }
@@ -775,10 +775,8 @@ int fr_dev_blind_rotate_multi(fr_ctx* ctx, const uint64_t* in, const uint8_t* lu
 
 int fr_set_profiling(fr_ctx* ctx, int32_t on) {
     FR_TRY({
-        NEED(ctx);
-        // 0 off, 2 the keyswitch timers too; any other nonzero value is level 1 (the
-        // function took a boolean before the levels existed)
-        ctx->device().set_profiling(on == 2 ? 2 : (on ? 1 : 0));
+        NEED(ctx && on >= 0 && on <= 2);  // 0 off, 1 blind-rotation timers, 2 the keyswitch timers too
+        ctx->device().set_profiling(on);
     })
 }
 

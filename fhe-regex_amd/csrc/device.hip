@@ -1713,7 +1713,7 @@ void Device::launch_level(const DevGate* d_gates, const DevGate* host, size_t n)
     if (profiling_) {
         t.gates = n;
         t.lat = latency_shape(n);
-        t.pair = pair_shape(n);
+        t.pair = pair_shape(n) && !fft_dual_;  // FR_FFT_DUAL launches: one bootstrap per workgroup
         t.ks = profiling_ >= 2;
         t.outs = 0;
         for (size_t i = 0; i < n; ++i) t.outs += host[i].n_out;

@@ -857,6 +857,10 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         constexpr int G_L2 = !LAT ? 3 : B > 1 ? (NPF + 1 < 3 ? NPF + 1 : 3) : G_TOP == 3 ? NPF : G_TOP + 2 < 3 ? G_TOP + 2 : 3;
         constexpr int PH_L1 = B > 1 ? FR_PAIR_LOAD : FR_LAT_LOAD1;
         constexpr int PH_L2 = B > 1 ? FR_PAIR_LOAD2 : FR_LAT_LOAD2;
+        // a group loaded after a forward phase needs that phase to exist: an out-of-range
+        // -D knob would skip the load and leave the MAC reading stale key registers
+        static_assert(G_L1 >= 3 || PH_L1 < G::NPH, "FR_PAIR_LOAD / FR_LAT_LOAD1 past the last forward phase");
+        static_assert(G_L2 >= 3 || PH_L2 < G::NPH, "FR_PAIR_LOAD2 / FR_LAT_LOAD2 past the last forward phase");
         if constexpr (G_TOP < 3) {
             __builtin_amdgcn_sched_barrier(0);
             load_ggsw(G_TOP, t);

@@ -4,6 +4,7 @@
 #include <algorithm>
 #include <bitset>
 #include <map>
+#include <queue>
 #include <tuple>
 #include <cstring>
 #include <iterator>
@@ -461,6 +462,159 @@ struct Lowerer {
         }
         return memo[id];
     }
+
+    // ---------------------------------------------------------- faithful tree
+    // The faithful gates with the reference's AND/OR chains rebalanced.
+    // A chain is a maximal run of AND (or OR) nodes in which every inner node is used
+    // once, by the next node of the same op: the left fold of has_match
+    // (engine.rs:22-35) and the Seq / Repeated AND chains (engine.rs:127-211).  A chain
+    // over m operands keeps exactly m - 1 two-input gates, as lower_f makes one per node
+    // (the reference's PBS count), but they form a tree of least depth: the two
+    // shallowest operands are joined first (ties in operand order).  A constant operand
+    // (or(false, x) is not short-circuited, execution.rs:154-164) is joined to the
+    // shallowest other operand as the same trivial-offset gate lower_f makes.
+    std::vector<int32_t> glv;  // level of each gate (1 + its deepest gate input)
+    int gate_level(int g) {
+        for (int i = (int)glv.size(); i <= g; ++i) {
+            int l = 0;
+            for (const PIn& in : prog.gates[i].ins)
+                if (in.src >= 0) l = std::max(l, glv[in.src]);
+            glv.push_back(l + 1);
+        }
+        return glv[g];
+    }
+    struct Item {
+        bool is_const;
+        int c;
+        Lit lit;
+    };
+    int pair_gate(bool is_and, const Item& p, const Item& q, int chain, int k) {
+        PGate g;
+        int offset = 0;
+        for (const Item* o : {&p, &q}) {
+            if (o->is_const) {
+                offset += o->c;
+            } else {
+                g.ins.push_back({o->lit.gate, o->lit.neg ? -1 : 1});
+                offset += o->lit.neg;
+            }
+        }
+        g.offset = 2 * offset;
+        if (is_and) lut_eq(g.lut, 2);
+        else lut_at_least(g.lut, 1);
+        return add_gate({9, is_and, chain, k}, std::move(g));
+    }
+    Form lower_ft(int id) {
+        const size_t nn = dag.nodes.size();
+        std::vector<int32_t> nuse(nn, 0), user(nn, -1);
+        for (size_t x = 0; x < nn; ++x) {
+            const VNode& n = dag.nodes[x];
+            if (n.op == VNode::AND || n.op == VNode::OR) {
+                ++nuse[n.a], user[n.a] = (int)x;
+                ++nuse[n.b], user[n.b] = (int)x;
+            } else if (n.op == VNode::NOT) {
+                ++nuse[n.a], user[n.a] = (int)x;
+            }
+        }
+        ++nuse[id];  // the root is used by the result
+        auto absorbed = [&](int x) {
+            const VNode& n = dag.nodes[x];
+            return (n.op == VNode::AND || n.op == VNode::OR) && nuse[x] == 1 && user[x] >= 0 &&
+                   dag.nodes[user[x]].op == n.op;
+        };
+        std::vector<int> st{id};
+        while (!st.empty()) {
+            int x = st.back();
+            if (done[x]) { st.pop_back(); continue; }
+            const VNode& n = dag.nodes[x];
+            bool ready = true;
+            if ((n.op == VNode::AND || n.op == VNode::OR || n.op == VNode::NOT)) {
+                if (!done[n.a]) { st.push_back(n.a); ready = false; }
+                if (n.b >= 0 && !done[n.b]) { st.push_back(n.b); ready = false; }
+            }
+            if (!ready) continue;
+            st.pop_back();
+            Form f;
+            switch (n.op) {
+                case VNode::POS: throw Error(FR_ERR_INVALID, "lowering: content char used as a boolean");
+                case VNode::CONST: f = const_form(n.c); break;
+                case VNode::EQ:
+                case VNode::GT:
+                case VNode::LE:
+                    lower_f(x);  // the comparison gates are lower_f's (it fills memo[x], done[x])
+                    continue;
+                case VNode::NOT: f = negate(memo[n.a]); break;
+                case VNode::AND:
+                case VNode::OR: {
+                    if (absorbed(x)) break;  // an inner link: its chain root gathers its operands
+                    const bool is_and = n.op == VNode::AND;
+                    // the chain's operands, left to right
+                    std::vector<Item> leaves;
+                    std::vector<int> ds{n.b, n.a};
+                    while (!ds.empty()) {
+                        int y = ds.back();
+                        ds.pop_back();
+                        if (absorbed(y) && user[y] >= 0) {
+                            ds.push_back(dag.nodes[y].b);
+                            ds.push_back(dag.nodes[y].a);
+                            continue;
+                        }
+                        const Form& o = memo[y];
+                        if (o.k == Form::CONST) leaves.push_back(Item{true, o.c, Lit{-1, false}});
+                        else leaves.push_back(Item{false, 0, materialize(o)});
+                    }
+                    // least-depth binary tree: join the two shallowest operands first
+                    using QE = std::tuple<int, int, int>;  // (level, order, item index)
+                    std::priority_queue<QE, std::vector<QE>, std::greater<QE>> q;
+                    std::vector<Item> items;
+                    std::vector<Item> consts;
+                    int order = 0;
+                    for (const Item& it : leaves) {
+                        if (it.is_const) { consts.push_back(it); continue; }
+                        items.push_back(it);
+                        q.emplace(gate_level(it.lit.gate), order++, (int)items.size() - 1);
+                    }
+                    int k = 0;
+                    auto join = [&](const Item& p, const Item& r) {
+                        int g = pair_gate(is_and, p, r, x, k++);
+                        items.push_back(Item{false, 0, Lit{g, false}});
+                        q.emplace(gate_level(g), order++, (int)items.size() - 1);
+                    };
+                    size_t c0 = 0;
+                    if (q.empty()) {
+                        // every operand's value is a constant (a short-circuit returns its
+                        // operand under a new key, execution.rs:121-164, so the op above it is
+                        // real): lower_f's input-free gate, as the first join
+                        if (consts.size() < 2) throw Error(FR_ERR_INVALID, "lowering: one-operand chain");
+                        join(consts[0], consts[1]);
+                        c0 = 2;
+                    }
+                    for (size_t ci = c0; ci < consts.size(); ++ci) {
+                        const Item& c = consts[ci];
+                        auto [lv, od, ix] = q.top();
+                        q.pop();
+                        (void)lv, (void)od;
+                        join(items[ix], c);
+                    }
+                    while (q.size() > 1) {
+                        auto [l1, o1, i1] = q.top();
+                        q.pop();
+                        auto [l2, o2, i2] = q.top();
+                        q.pop();
+                        (void)l1, (void)l2;
+                        // operand order as in the chain (the earlier one first)
+                        if (o1 < o2) join(items[i1], items[i2]);
+                        else join(items[i2], items[i1]);
+                    }
+                    f = lit_form(items[std::get<2>(q.top())].lit);
+                    break;
+                }
+            }
+            memo[x] = std::move(f);
+            done[x] = 1;
+        }
+        return memo[id];
+    }
 };
 
 }  // namespace
@@ -484,7 +638,8 @@ void compute_levels(Program& prog) {
 
 Program lower(const ValueDag& dag, int root, int mode) {
     Lowerer lw(dag, mode);
-    Form f = mode == FR_LOWER_FAITHFUL ? lw.lower_f(root) : lw.lower_t(root);
+    Form f = mode == FR_LOWER_FAITHFUL ? lw.lower_f(root)
+             : mode == FR_LOWER_FAITHFUL_TREE ? lw.lower_ft(root) : lw.lower_t(root);
     if (f.k == Form::CONST) {
         lw.prog.out_gate = -1;
         lw.prog.out_const = f.c;

@@ -31,7 +31,7 @@ HEADER = os.path.join(REPO, "include", "fheregex.h")
 
 FR_OK = 0
 ERR_INVALID, ERR_PARSE, ERR_REF_PANIC, ERR_NO_DEVICE, ERR_HIP, ERR_NO_KEY, ERR_OOM, ERR_NON_ASCII = range(-1, -9, -1)
-LOWER_FAITHFUL, LOWER_THRESHOLD = 0, 1
+LOWER_FAITHFUL, LOWER_THRESHOLD, LOWER_FAITHFUL_TREE = 0, 1, 2
 ENGINE_AUTO, ENGINE_ENUMERATE, ENGINE_MERGED = 0, 1, 2
 GRAMMAR_REFERENCE, GRAMMAR_EXT = 0, 1
 KEYGEN_AUTO, KEYGEN_HOST, KEYGEN_DEVICE = 0, 1, 2

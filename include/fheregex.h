@@ -347,8 +347,14 @@ int fr_set_engine(fr_ctx* ctx, int32_t engine);
 int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                       int32_t lowering, int32_t engine, fr_plain_result* out);
 
-/* lowering modes for fr_plain_match / fr_set_lowering */
-enum { FR_LOWER_FAITHFUL = 0, FR_LOWER_THRESHOLD = 1 };
+/* lowering modes for fr_plain_match / fr_set_lowering:
+ * FR_LOWER_FAITHFUL: one gate group per reference op (eq/gt/le = 3 PBS, and/or = 1,
+ *   not linear), in the reference's fold order (engine.rs:22-35: depth #branches).
+ * FR_LOWER_THRESHOLD (default): threshold gates of fan-in <= 16, multi-value LUTs.
+ * FR_LOWER_FAITHFUL_TREE: FR_LOWER_FAITHFUL's gates, the same PBS count, with every
+ *   AND/OR chain whose inner links are used once rebalanced into a binary tree of
+ *   least depth (/abc/ x 256: 3,047 PBS in 13 levels, not 257). */
+enum { FR_LOWER_FAITHFUL = 0, FR_LOWER_THRESHOLD = 1, FR_LOWER_FAITHFUL_TREE = 2 };
 int fr_set_lowering(fr_ctx* ctx, int32_t mode);
 /* Multi-value bootstrapping: gates of one level that read the same linear
  * combination share one blind rotation (default on). */
@@ -359,7 +365,7 @@ int fr_set_multi_value(fr_ctx* ctx, int32_t on);
  * included; what bench.py's timed region uses; FR_TIMER_CHAIN=0 stamps a start event on
  * the blind rotation instead, 9-15 us more per launch); 2 also the keyswitch timers (start
  * and stop events on every level's keyswitch, ~30 us per /abc/ x 256 match).  Timers
- * resolve at the next synchronisation.  Any nonzero value other than 2 is level 1. */
+ * resolve at the next synchronisation.  Any other value is FR_ERR_INVALID. */
 int fr_set_profiling(fr_ctx* ctx, int32_t on);
 
 /* ----- single-stage device entry points (parity tests of each kernel) ----- */

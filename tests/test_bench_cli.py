@@ -67,6 +67,54 @@ def test_mode_defaults():
         bench.resolve_mode("weak", "starts", 2, 4)
 
 
+def test_n_gt_1_defaults_measure_named_lengths():
+    """N > 1 defaults per workload: the metric's value is weak start shards
+    (N x 256 chars, the named 256 split as the `strong_starts` record); config 4's value is
+    its named 1,024 chars split by start offsets; the anchored configs split one match by
+    closures.  Explicit flags win."""
+    import bench
+    assert bench.default_mode("metric", "", "") == ("weak", "starts")
+    assert bench.default_mode("config4", "", "") == ("strong", "starts")
+    assert bench.default_mode("config5", "", "") == ("strong", "closure")
+    assert bench.default_mode("config3", "", "") == ("strong", "closure")
+    assert bench.default_mode("config4", "weak", "") == ("weak", "")
+    assert bench.default_mode("config4", "", "closure") == ("strong", "closure")
+    assert bench.resolve_mode(*bench.default_mode("config4", "", ""), 8, 1) == (True, "starts")
+    assert bench.resolve_mode(*bench.default_mode("config5", "", ""), 8, 1) == (True, "closure")
+    assert bench.resolve_mode(*bench.default_mode("metric", "", ""), 8, 1) == (False, "starts")
+
+
+def test_nccl_device_guard():
+    """Under nccl every local rank needs its own GPU (RCCL refuses two ranks on one
+    device); gloo rehearsals may share one"""
+    import bench
+    assert bench.nccl_device_guard("nccl", 2, 1) and "one GPU per rank" in bench.nccl_device_guard("nccl", 2, 1)
+    assert bench.nccl_device_guard("nccl", 8, 8) is None
+    assert bench.nccl_device_guard("gloo", 4, 1) is None
+
+
+def test_nccl_ranks_beyond_devices_exit_nonzero():
+    """`--gpus 2` under nccl where fewer GPUs are visible (here: none) ends every rank
+    with the guard's message and a non-zero status, before any collective"""
+    res = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--steps", "1", "--warmup", "0"],
+                         capture_output=True, text=True, timeout=240, env=_env())
+    assert res.returncode != 0
+    assert "one GPU per rank" in res.stderr
+    assert not [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+
+
+def test_job_timeout_kills_stuck_ranks(tmp_path):
+    """--job-timeout: spawned ranks that outlive it are killed as a process group and the
+    launcher exits 124 (a stuck collective does not hold the node)"""
+    import bench
+    stub = tmp_path / "sleeper.py"
+    stub.write_text("import time\ntime.sleep(600)\n")
+    import time
+    t = time.time()
+    rc = bench.spawn_ranks(2, [], 3.0, script=str(stub))
+    assert rc == 124 and time.time() - t < 120
+
+
 @pytest.mark.gpu
 def test_one_rank_rccl_group_pipeline():
     """The N > 1 start-shard pipeline over a one-rank RCCL group on the GPU (bench.py

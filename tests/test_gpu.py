@@ -976,14 +976,16 @@ def test_export_async_and_or_each(gctx):
     import torch
     hs1 = gctx.upload_radix(gctx.encrypt_str("zzabczzzzz", seed=90))
     hs0 = gctx.upload_radix(gctx.encrypt_str("zzzzzzzzzz", seed=91))
-    buf = torch.zeros((4, gctx.lwe_len), dtype=torch.int64, device="cuda:0")
+    lib_stream = torch.cuda.ExternalStream(gctx.stream_ptr(), device=torch.device("cuda", 0))
+    buf = torch.empty((4, gctx.lwe_len), dtype=torch.int64, device="cuda:0")
+    lib_stream.wait_stream(torch.cuda.current_stream())  # the exports run after the allocation's work
     outs = []
     for i, hs in enumerate([hs1, hs0, hs0, hs1]):
         o, _ = gctx.has_match(hs, "/abc/")
         gctx.export_bool_device_async([o], buf[i].data_ptr())
         outs.append(o)
     ev = torch.cuda.Event()
-    ev.record(torch.cuda.ExternalStream(gctx.stream_ptr(), device=torch.device("cuda", 0)))
+    ev.record(lib_stream)
     ev.synchronize()
     ref = torch.zeros_like(buf)
     gctx.export_bool_device(outs, ref.data_ptr())
@@ -1018,23 +1020,45 @@ def test_match_words_full_size_configs(gctx, oracle_k1, which):
     assert got == exp == 1
 
 
-@pytest.mark.parametrize("variant", ["faithful", "no-multi-value"])
+@pytest.mark.parametrize("variant", ["faithful", "faithful_tree", "no-multi-value"])
 def test_match_words_lowering_variants(gctx, oracle_k1, variant):
     """The reference-structured lowering (FR_LOWER_FAITHFUL: one gate group per smart_*
-    op, execution.rs:64-195; 743 PBS for /abc/ x 64) and the threshold lowering without
-    multi-value bootstrapping, word for word against the oracle's schedule evaluation."""
+    op, execution.rs:64-195; 743 PBS for /abc/ x 64), the same gates with the fold's
+    AND/OR chains rebalanced (FR_LOWER_FAITHFUL_TREE: 743 PBS in 10 levels instead of 65)
+    and the threshold lowering without multi-value bootstrapping, word for word against
+    the oracle's schedule evaluation."""
     rng = np.random.default_rng(41)
     s = _printable(rng, 64).replace("abc", "abd")
     s = s[:20] + "abc" + s[23:]
-    if variant == "faithful":
-        gctx.set_lowering(F.LOWER_FAITHFUL)
-    else:
+    mode = {"faithful": F.LOWER_FAITHFUL, "faithful_tree": F.LOWER_FAITHFUL_TREE}.get(variant, F.LOWER_THRESHOLD)
+    gctx.set_lowering(mode)
+    if variant == "no-multi-value":
         gctx.set_multi_value(False)
     try:
-        got = _match_words_vs_oracle(gctx, oracle_k1, s, "/abc/", 42,
-                                     lowering=F.LOWER_FAITHFUL if variant == "faithful" else F.LOWER_THRESHOLD,
+        got = _match_words_vs_oracle(gctx, oracle_k1, s, "/abc/", 42, lowering=mode,
                                      multi_value=variant != "no-multi-value")
     finally:
         gctx.set_lowering(F.LOWER_THRESHOLD)
         gctx.set_multi_value(True)
     assert got == 1
+
+
+def test_faithful_tree_full_metric(gctx, oracle_k1):
+    """FR_LOWER_FAITHFUL_TREE on the metric workload (/abc/ x 256): the reference's 3,047
+    PBS in 12 levels, word for word against the oracle's schedule evaluation"""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    content = bench.make_content("printable", 256, seed=3).decode()
+    gctx.set_lowering(F.LOWER_FAITHFUL_TREE)
+    try:
+        got = _match_words_vs_oracle(gctx, oracle_k1, content, "/abc/", 4321, lowering=F.LOWER_FAITHFUL_TREE)
+        hs = gctx.upload_radix(gctx.encrypt_str(content, seed=4322))
+        out, st = gctx.has_match(hs, "/abc/")
+        assert gctx.decrypt_radix(gctx.download_radix(out)) == 1
+        for h in hs + [out]:
+            gctx.release(h)
+    finally:
+        gctx.set_lowering(F.LOWER_THRESHOLD)
+    assert got == 1
+    assert (st.pbs, st.levels) == (3047, 12)

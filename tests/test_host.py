@@ -38,12 +38,24 @@ def test_host_only_context_fails_loudly_on_gpu_ops(key_blob):
         ctx.dev_ring_mul(np.zeros(2048, np.uint64), np.zeros(2048, np.uint64))
 
 
+def test_set_profiling_rejects_invalid_levels():
+    """fr_set_profiling takes 0, 1 or 2; anything else is FR_ERR_INVALID,
+    checked before the device, so a host-only context sees it too"""
+    ctx = F.Context(device=-1)
+    for bad in (-1, 3, 255):
+        with pytest.raises(F.FheRegexError) as e:
+            ctx.set_profiling(bad)
+        assert not isinstance(e.value, F.NoDevice)
+    with pytest.raises(F.NoDevice):
+        ctx.set_profiling(1)
+
+
 @pytest.mark.parametrize("v", load("parser_vectors.json"), ids=lambda v: v["pattern"])
 def test_parser_golden(v):
     assert F.parse(v["pattern"]) == v["ast"]
 
 
-@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD])
+@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD, F.LOWER_FAITHFUL_TREE])
 @pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
 def test_engine_golden(v, mode):
     r = F.plain_match(v["content"], v["pattern"], mode)
@@ -77,7 +89,7 @@ def test_fuzz_vs_oracle():
             exp, e_exc = None, type(e).__name__
         if exp is not None and exp.n_branches > 500:
             continue
-        for mode in (F.LOWER_FAITHFUL, F.LOWER_THRESHOLD):
+        for mode in (F.LOWER_FAITHFUL, F.LOWER_THRESHOLD, F.LOWER_FAITHFUL_TREE):
             try:
                 r = F.plain_match(c, p, mode)
                 got, g_exc = (r.result_recorded, r.result_lowered, r.ct_ops, r.cache_hits), None
@@ -99,6 +111,35 @@ def test_config_counts_and_pbs():
         assert (r.ct_ops, r.cache_hits, r.pbs) == (ops, 0, pbs), p
         t = F.plain_match(c, p, F.LOWER_THRESHOLD)
         assert t.ct_ops == ops and t.pbs < pbs and t.levels <= 6, (p, t.pbs, t.levels)
+
+
+def test_faithful_tree_keeps_the_reference_op_mix():
+    """FR_LOWER_FAITHFUL_TREE: the faithful gates (eq/gt/le = 3 PBS, and/or = 1), the same
+    PBS count as FR_LOWER_FAITHFUL on every pattern, with the AND/OR chains of the
+    reference's fold (engine.rs:22-35) rebalanced: log depth instead of #branches"""
+    cases = [("abc", "/^abc$/", 11, 5), ("x" * 64, "/abc/", 743, 10), ("x" * 256, "/abc/", 3047, 12),
+             ("b" * 256, "/^[a-z]+$/", 2047, 12), ("x" * 1024, "/the/i", 24527, 15)]
+    for c, p, pbs, levels in cases:
+        f = F.plain_match(c, p, F.LOWER_FAITHFUL)
+        t = F.plain_match(c, p, F.LOWER_FAITHFUL_TREE)
+        assert (t.ct_ops, t.pbs) == (f.ct_ops, f.pbs) == (t.ct_ops, pbs), p
+        assert t.levels <= levels and t.levels <= f.levels, (p, t.levels, f.levels)
+        assert t.result_lowered == f.result_lowered == f.result_recorded
+    rng = random.Random(23)
+    n = 0
+    while n < 300:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(1, 10))
+        try:
+            f = F.plain_match(c, p, F.LOWER_FAITHFUL)
+        except (F.ParseError, F.ReferencePanic):
+            continue
+        if f.n_branches > 500:
+            continue
+        t = F.plain_match(c, p, F.LOWER_FAITHFUL_TREE)
+        assert (t.pbs, t.result_lowered) == (f.pbs, f.result_recorded), (c, p)
+        assert t.levels <= f.levels, (c, p, t.levels, f.levels)
+        n += 1
 
 
 @pytest.mark.parametrize("content,pattern", [("q" * 100 + "abc" + "q" * 40, "/abc/"), ("b" * 90 + "z", "/^[a-z]+$/"),
@@ -169,7 +210,7 @@ def test_product_encrypt_matches_oracle(key_blob, oracle_k1):
 
 # --- state-merging engine -------------------------------
 
-@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD])
+@pytest.mark.parametrize("mode", [F.LOWER_FAITHFUL, F.LOWER_THRESHOLD, F.LOWER_FAITHFUL_TREE])
 @pytest.mark.parametrize("v", load("engine_vectors.json"), ids=lambda v: f'{v["content"]!r}-{v["pattern"]}')
 def test_merged_engine_golden(v, mode):
     r = F.plain_match(v["content"], v["pattern"], mode, engine=F.ENGINE_MERGED)
