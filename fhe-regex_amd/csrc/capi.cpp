@@ -18,6 +18,9 @@
 
 namespace fr {
 
+// PARAM_MESSAGE_2_CARRY_2 (ciphertext.rs:1): 2-bit message, 2-bit carry per block
+constexpr uint64_t MESSAGE_MODULUS = 4, CARRY_MODULUS = 4;
+
 static thread_local std::string g_last_error;
 void set_last_error(const std::string& m) { g_last_error = m; }
 
@@ -794,6 +797,11 @@ int fr_load_client_key(fr_ctx* ctx, const uint8_t* data, size_t len) {
         ClientKey ck = parse_client_key(data, len);
         if ((size_t)ctx->p.k * ctx->p.N != ck.s_big.size() || (size_t)ctx->p.n != ck.s_small.size())
             throw Error(FR_ERR_INVALID, "client key dimensions do not match the context params");
+        // the radix encoding this build implements: PARAM_MESSAGE_2_CARRY_2, 4 blocks per
+        // character (ciphertext.rs:1,12-13,43-44); a key of other parameters would decode wrong
+        if (ck.message_modulus != MESSAGE_MODULUS || ck.carry_modulus != CARRY_MODULUS || ck.num_blocks != 4)
+            throw Error(FR_ERR_INVALID, "client key: message/carry modulus or block count other than "
+                                        "PARAM_MESSAGE_2_CARRY_2 with 4 blocks");
         ctx->ck = std::move(ck);
         ctx->has_ck = true;
         ctx->has_sk = false;
@@ -861,8 +869,6 @@ int fr_encrypt_blocks(fr_ctx* ctx, const uint8_t* msgs, size_t count, uint64_t s
 }
 
 // radix messages of a string (ciphertext.rs:18-29: 4 blocks of 2 bits, least significant first)
-// PARAM_MESSAGE_2_CARRY_2 (the only parameter family of the reference)
-constexpr uint64_t MESSAGE_MODULUS = 4, CARRY_MODULUS = 4;
 
 static std::vector<uint8_t> str_blocks(const char* s, size_t len) {
     std::vector<uint8_t> msgs(4 * len);
@@ -1602,7 +1608,9 @@ int fr_schedule_match(size_t n_chars, const char* pattern, size_t lo, size_t hi,
         if (jobs) {
             NEED(jobs_cap >= S.jobs.size());
             static_assert(sizeof(fr_job) == sizeof(DevGate), "fr_job mirrors DevGate");
-            std::memcpy(jobs, S.jobs.data(), sizeof(DevGate) * S.jobs.size());
+            // (an empty schedule's vector has no storage: memcpy's source must not be null,
+            // UBSan finding of tests/test_fuzz_inputs.py)
+            if (!S.jobs.empty()) std::memcpy(jobs, S.jobs.data(), sizeof(DevGate) * S.jobs.size());
         }
         if (level_off) {
             NEED(level_cap >= S.level_off.size());

@@ -60,8 +60,10 @@ static inline uint64_t pow_mod(uint64_t b, uint64_t e, uint64_t p) {
 // ---------------------------------------------------------------- key parse
 ClientKey parse_client_key(const uint8_t* d, size_t len) {
     size_t off = 0;
+    // bounds checks written so that no sum can wrap: a length field of the blob is caller
+    // data and may hold any 64-bit value
     auto u = [&](size_t o) -> uint64_t {
-        if (o + 8 > len) throw Error(FR_ERR_INVALID, "client key: truncated");
+        if (o > len || len - o < 8) throw Error(FR_ERR_INVALID, "client key: truncated");
         uint64_t v;
         std::memcpy(&v, d + o, 8);
         return v;
@@ -75,17 +77,21 @@ ClientKey parse_client_key(const uint8_t* d, size_t len) {
     ClientKey ck;
     uint64_t nb = u(off);
     if (nb == 0 || nb > (1u << 20)) throw Error(FR_ERR_INVALID, "client key: bad big key length");
+    if (nb > (len - 8) / 8) throw Error(FR_ERR_INVALID, "client key: truncated");
     ck.s_big.resize(nb);
     for (uint64_t i = 0; i < nb; ++i) ck.s_big[i] = u(off + 8 + 8 * i);
     off += 8 + 8 * nb;
     uint64_t ng = u(off);
+    if (ng > (len - off - 8) / 8) throw Error(FR_ERR_INVALID, "client key: truncated");
     off += 8 + 8 * ng;                 // GLWE key data (identical to the big key)
     off += 8;                          // polynomial_size
     uint64_t ns = u(off);
     if (ns == 0 || ns > (1u << 16)) throw Error(FR_ERR_INVALID, "client key: bad small key length");
+    if (ns > (len - off - 8) / 8) throw Error(FR_ERR_INVALID, "client key: truncated");
     ck.s_small.resize(ns);
     for (uint64_t i = 0; i < ns; ++i) ck.s_small[i] = u(off + 8 + 8 * i);
     off += 8 + 8 * ns;
+    if (u(off) != ns) throw Error(FR_ERR_INVALID, "client key: inconsistent dimensions");
     ck.n = (int)u(off);
     ck.k = (int)u(off + 8);
     ck.N = (int)u(off + 16);

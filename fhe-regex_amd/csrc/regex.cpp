@@ -96,10 +96,45 @@ struct PR {
 inline PR ok(ReP n, size_t p) { PR r; r.ok = true; r.pos = p; r.node = std::move(n); return r; }
 inline PR fail(bool committed) { PR r; r.committed = committed; return r; }
 
+// Nesting limit of the parser (groups, bracket negations): the recursive descent below,
+// like the reference's combine parser, takes stack per level, so a hostile pattern could
+// exhaust the caller's stack; past this depth the pattern is refused (FR_ERR_INVALID, a
+// limit of this build: the reference would overflow its stack instead).
+constexpr int MAX_NEST = 512;
+
 struct Parser {
     const std::string& s;
     const bool ext;  // FR_GRAMMAR_EXT
-    Parser(const std::string& str, bool e) : s(str), ext(e) {}
+    // Packrat memo: regex/term/factor/atom are pure functions of the position, but the
+    // reference's grammar tries atom up to four times per factor (attempt(atom '?'),
+    // three attempts of repeated, atom) and term twice per regex, so a plain recursive
+    // descent takes ~5^depth calls on nested groups ("((((((((((a))))))))))" ~10^7, as
+    // the reference does); memoised, every (rule, position) is parsed once.
+    std::vector<PR> m_regex, m_term, m_factor, m_atom;
+    std::vector<char> h_regex, h_term, h_factor, h_atom;
+    int depth = 0;
+    Parser(const std::string& str, bool e)
+        : s(str), ext(e), m_regex(str.size() + 1), m_term(str.size() + 1), m_factor(str.size() + 1),
+          m_atom(str.size() + 1), h_regex(str.size() + 1, 0), h_term(str.size() + 1, 0),
+          h_factor(str.size() + 1, 0), h_atom(str.size() + 1, 0) {}
+    struct Nest {  // one nesting level (restored on every exit)
+        int& d;
+        explicit Nest(int& dd) : d(dd) {
+            if (++d > MAX_NEST)
+                throw Error(FR_ERR_INVALID, "pattern nests deeper than " + std::to_string(MAX_NEST) + " levels");
+        }
+        ~Nest() { --d; }
+    };
+    template <class Fn>
+    PR memo(std::vector<PR>& m, std::vector<char>& h, size_t i, Fn&& fn) {
+        if (i < h.size() && h[i]) return m[i];
+        PR r = fn();
+        if (i < h.size()) {
+            m[i] = r;
+            h[i] = 1;
+        }
+        return r;
+    }
     bool at(size_t i, char ch) const { return i < s.size() && s[i] == ch; }
     static bool letter(unsigned char c) { return (c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z'); }
     static bool nonesc(unsigned char c) {  // parser.rs:252-254
@@ -123,6 +158,10 @@ struct Parser {
 
     // regex := attempt(term '|' regex) | term           (parser.rs:208-222)
     PR regex(size_t i) {
+        return memo(m_regex, h_regex, i, [&] { return regex_(i); });
+    }
+    PR regex_(size_t i) {
+        Nest nest(depth);
         PR t = term(i);
         if (t.ok && at(t.pos, '|')) {
             PR r = regex(t.pos + 1);
@@ -138,6 +177,9 @@ struct Parser {
     }
     // term := many(factor); one factor is returned unwrapped (parser.rs:224-236)
     PR term(size_t i) {
+        return memo(m_term, h_term, i, [&] { return term_(i); });
+    }
+    PR term_(size_t i) {
         std::vector<ReP> xs;
         size_t j = i;
         for (;;) {
@@ -157,6 +199,9 @@ struct Parser {
     }
     // factor := attempt(atom '?') | attempt(repeated) | atom   (parser.rs:238-250)
     PR factor(size_t i) {
+        return memo(m_factor, h_factor, i, [&] { return factor_(i); });
+    }
+    PR factor_(size_t i) {
         {
             PR a = atom(i);
             if (a.ok && at(a.pos, '?')) {
@@ -174,6 +219,9 @@ struct Parser {
     }
     // atom (parser.rs:256-269)
     PR atom(size_t i) {
+        return memo(m_atom, h_atom, i, [&] { return atom_(i); });
+    }
+    PR atom_(size_t i) {
         if (at(i, '.')) return ok(mk(Re::ANY), i + 1);
         if (at(i, '\\') && i + 1 < s.size()) return ok(mk_char((uint8_t)s[i + 1]), i + 2);
         if (i < s.size() && (letter((unsigned char)s[i]) || nonesc((unsigned char)s[i])))
@@ -199,6 +247,7 @@ struct Parser {
     // range (parser.rs:279-294)
     PR range(size_t i) {
         if (at(i, '^')) {
+            Nest nest(depth);
             PR r = range(i + 1);
             if (!r.ok) return fail(true);
             auto q = std::make_shared<Re>();
@@ -235,6 +284,7 @@ struct Parser {
     }
     PR ext_class(size_t i) {
         if (at(i, '^')) {
+            Nest nest(depth);
             PR r = ext_class(i + 1);
             if (!r.ok) return fail(true);
             auto q = std::make_shared<Re>();

@@ -26,31 +26,54 @@ constexpr int LANES = 512;
 constexpr int PER_LANE = 8;                                   // 16-byte loads per lane per group
 constexpr size_t GROUP_BYTES = (size_t)LANES * PER_LANE * 16;  // 64 KB
 
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+struct Grp {
+    v4u v[PER_LANE];
+};
+
+// one group's loads: raw buffer loads as the product's key loads (resource in SGPRs, the
+// group's byte offset uniform in soffset, one lane offset VGPR): 8 x dwordx4 per lane
+__device__ __forceinline__ void load_grp(Grp& g, __amdgpu_buffer_rsrc_t r, int lane_off, int grp) {
+    const int soff = __builtin_amdgcn_readfirstlane(grp) * (int)GROUP_BYTES;
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i)
+        g.v[i] = __builtin_amdgcn_raw_buffer_load_b128(r, lane_off + i * LANES * 16, soff, 0);
+}
+template <int W>
+__device__ __forceinline__ void consume(const Grp& g, double& acc) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < PER_LANE; ++i)
+        s += __hiloint2double((int)g.v[i].y, g.v[i].x) + __hiloint2double((int)g.v[i].w, g.v[i].z);
+    // one serial chain through acc (at least one fma): the compiler cannot move a group's
+    // consumption past the next group's loads
+#pragma unroll
+    for (int w = 0; w < (W > 0 ? W : 1); ++w) acc = fma(acc, 0.999999, s);
+}
+
 template <int D, int W>
 __global__ void __launch_bounds__(LANES) k_stream(const uint4* __restrict__ key, int groups, double* out) {
     extern __shared__ char lds_pad[];  // dynamic LDS: one workgroup per CU
     const int tl = threadIdx.x;
-    uint4 buf[D][PER_LANE];
+    const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)key, 0, 0x7fffffff, 0x00020000);
+    const int lane_off = tl * 16;
+    Grp g[D];
     double acc = (double)tl;
-    auto load = [&](int d, int g) {
-        const uint4* p = key + (size_t)g * (LANES * PER_LANE) + tl;
 #pragma unroll
-        for (int i = 0; i < PER_LANE; ++i) buf[d][i] = p[i * LANES];  // default cache policy, as the product's key loads
-    };
-#pragma unroll
-    for (int d = 0; d < D; ++d) load(d, d);
+    for (int d = 0; d < D; ++d) {
+        load_grp(g[d], r, lane_off, d);
+        __builtin_amdgcn_sched_barrier(0);
+    }
     for (int g0 = 0; g0 < groups; g0 += D) {
 #pragma unroll
         for (int d = 0; d < D; ++d) {
-            double s = 0.0;
-#pragma unroll
-            for (int i = 0; i < PER_LANE; ++i)
-                s += __hiloint2double((int)buf[d][i].y, buf[d][i].x) + __hiloint2double((int)buf[d][i].w, buf[d][i].z);
-#pragma unroll
-            for (int w = 0; w < W; ++w) acc = fma(acc, 0.999999, s);
-            if (W == 0) acc += s;
+            // the ring's order is fixed (sched barriers): consuming group d waits for its
+            // own loads only, the other D - 1 groups stay in flight
+            consume<W>(g[d], acc);
+            __builtin_amdgcn_sched_barrier(0);
             const int nxt = g0 + D + d;
-            load(d, nxt < groups ? nxt : 0);
+            load_grp(g[d], r, lane_off, nxt < groups ? nxt : 0);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     if (acc == 1234.5) out[blockIdx.x * LANES + tl] = acc + lds_pad[tl];
@@ -103,10 +126,10 @@ int main() {
     CK(hipMalloc(&out, (size_t)256 * LANES * sizeof(double)));
     CK(hipMemset(key, 0x3f, bytes));
     int rc = 0;
-    rc |= row<1, 0>(key, out, "ring 1, no work");
-    rc |= row<2, 0>(key, out, "ring 2, no work");
-    rc |= row<3, 0>(key, out, "ring 3, no work");
-    rc |= row<4, 0>(key, out, "ring 4, no work");
+    rc |= row<1, 0>(key, out, "ring 1, 1 fma/group");
+    rc |= row<2, 0>(key, out, "ring 2, 1 fma/group");
+    rc |= row<3, 0>(key, out, "ring 3, 1 fma/group");
+    rc |= row<4, 0>(key, out, "ring 4, 1 fma/group");
     rc |= row<3, 48>(key, out, "ring 3, 48 fma/group");
     rc |= row<4, 48>(key, out, "ring 4, 48 fma/group");
     rc |= row<3, 96>(key, out, "ring 3, 96 fma/group");
