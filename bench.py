@@ -62,6 +62,15 @@ import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "fhe-regex_amd"))
+# hardware queues per process (read at HIP init): the `inflight_1ctx` record's lanes are
+# streams of one context, and with HIP's default of 4 two of four lanes share a queue and
+# serialise (tools/lanes_probe.py: 4 lanes 5.44 ms per match with 4 queues, 4.22 with 8); the
+# timed single-stream match is unaffected
+try:
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+except ValueError:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402
 
@@ -430,6 +439,9 @@ def main():
     ap.add_argument("--inflight", type=int, default=3,
                     help="N=1: secondary record of C matches in flight on C contexts (streams) of the GPU, "
                          "dealt round-robin (0: skip)")
+    ap.add_argument("--lanes", type=int, default=4,
+                    help="N=1: secondary record of matches in flight on the lanes (streams) of ONE context with one "
+                         "key (fr_set_lanes; 0: skip)")
     ap.add_argument("--faithful-steps", type=int, default=1,
                     help="N=1 metric: timed matches of the reference-structured lowering (FR_LOWER_FAITHFUL) "
                          "for the `faithful` sub-record (0: skip)")
@@ -920,6 +932,34 @@ def main():
         for c in ictx[1:]:
             c.close()
 
+    inflight_1ctx = None
+    if args.lanes > 1 and world == 1 and M == 1 and rank == 0 and not starts:
+        # serving with ONE key: the same matches in flight on the lanes (streams) of this
+        # context (fr_set_lanes), each lane its own plan copy; consecutive asynchronous
+        # matches round-robin over the lanes, so a match's small levels share the chip with
+        # the next match's first level
+        ctx.set_lanes(args.lanes)
+        try:
+            for _ in range(args.lanes):  # each lane's plan
+                ctx.release(ctx.has_match(handles_np, pattern)[0])
+            torch.cuda.synchronize()
+            ctx.download_radix(handles[next(i for i, h in enumerate(handles) if h != F.NULL_CT)])
+            nm = max(args.steps, 4 * args.lanes)
+            t = time.perf_counter()
+            outs_l = [ctx.has_match(handles_np, pattern)[0] for _ in range(nm)]
+            w_l = ctx.download_radix(outs_l[-1])  # synchronises every lane
+            lms = (time.perf_counter() - t) * 1e3 / nm
+            same = all(np.array_equal(ctx.download_radix(o)[0], words0) for o in outs_l) if words0 is not None else None
+            for o in outs_l:
+                ctx.release(o)
+        finally:
+            ctx.set_lanes(1)
+        inflight_1ctx = {"lanes": args.lanes, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES"), "matches": nm, "ms_per_match_amortised": lms,
+                         "value": rotations_per_match_local / (lms / 1e3), "unit": "gate-bootstraps/s",
+                         "bit_identical_to_timed_region": same, "result_decrypted": ctx.decrypt_radix(w_l),
+                         "note": "secondary, serving view with one key: matches in flight on the lanes (streams) of "
+                                 "one context (fr_set_lanes), each lane its own plan copy. Never `value`."}
+
     step_latency = None
     if starts:
         # latency of one start-sharded match end to end (match, export, gather, the OR on
@@ -1138,6 +1178,7 @@ def main():
         "results_ok_steps": starts_ok,
         "step_latency": step_latency,
         "inflight": inflight,
+        "inflight_1ctx": inflight_1ctx,
         "weak_matches": weak_matches,
         "faithful": faithful,
         "faithful_tree": faithful_tree,

@@ -87,6 +87,7 @@ struct fr_ctx {
     bool sk_on_device = false;  // server key generated on the device (export downloads it)
     bool multi_value = true;  // merge same-input small-norm LUTs into one blind rotation
     bool async_match = true;  // has_match returns once its launches are enqueued (fr_set_async)
+    uint64_t next_lane = 0;   // fr_set_lanes: consecutive asynchronous matches round-robin over the lanes
     fr_plan_cache* plans = nullptr;
     // content_signature scratch: canonical id of an arena slot, valid while sig_gen[slot] == gen
     std::vector<int32_t> sig_id;
@@ -530,8 +531,23 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
     std::string key;
     std::vector<int32_t> sig;
     std::vector<int> cmap;
+    // lanes (fr_set_lanes): an asynchronous match of a cacheable plan runs on the next lane,
+    // with a plan of its own (its intermediate slots), so consecutive matches overlap
+    const int lane =
+        (ctx->async_match && dev.match_lanes() > 0 && pc.capacity) ? 1 + (int)(ctx->next_lane++ % dev.match_lanes()) : 0;
+    struct LaneScope {  // left on every exit, exceptions included
+        Device& d;
+        bool in = false;
+        void enter(int i) {
+            if (i > 0) d.enter_lane(i), in = true;
+        }
+        ~LaneScope() {
+            if (in) d.leave_lane();
+        }
+    } lane_scope{dev};
     if (pc.capacity) {
         key = match_key(ctx, pattern, n, M, lo, hi);
+        if (lane) key += "|lane" + std::to_string(lane);
         sig = content_signature(ctx, content, n * M, &cmap);
         for (auto& e : pc.entries)
             if (e->key == key && e->sig == sig) hit = e.get();
@@ -544,6 +560,7 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
     if (hit) {
         ++pc.hits;
         hit->last_use = ++pc.clock;
+        lane_scope.enter(lane);
         dev.bind_content(cmap.data(), cmap.size());
         t1 = now_ms();
         launch_plan(dev, hit->plan);
@@ -607,6 +624,7 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
             CachedMatch& c = *e;
             pc.entries.push_back(std::move(e));
             c.plan.d_gates = dev.upload_gates(c.plan.gates.data(), c.plan.gates.size(), c.plan.n_refs);
+            lane_scope.enter(lane);
             dev.bind_content(cmap.data(), cmap.size());
             t1 = now_ms();
             launch_plan(dev, c.plan);
@@ -1269,6 +1287,14 @@ int fr_set_plan_cache(fr_ctx* ctx, size_t capacity) {
         NEED(ctx);
         ctx->plans->capacity = capacity;
         evict_for(ctx, 0, 0);  // drop the least recently used beyond the new capacity
+    })
+}
+
+int fr_set_lanes(fr_ctx* ctx, int32_t n) {
+    FR_TRY({
+        NEED(ctx && n >= 1 && n <= 8);
+        ctx->device().set_lanes(n);
+        ctx->next_lane = 0;
     })
 }
 

@@ -100,6 +100,17 @@ class Device {
     void run_linear(const DevGate& g);
     void sync();
 
+    // Lanes (serving without key copies): lane 0 is the stream above; lanes 1..n are
+    // further streams of this device with their own keyswitch / digit scratch and content
+    // map, sharing the keys and the arena.  Between enter_lane(i) and leave_lane() every
+    // launch goes to lane i's stream, ordered after everything enqueued on lane 0 so far.
+    // Work on lane 0 waits (device-side, by event) for every lane's enqueued work before it
+    // runs; slots freed while a lane may still read them return to the free list only after
+    // a host synchronisation of every lane (sync()).
+    void set_lanes(int n);                                 // n = 1: lane 0 only; n >= 2: lanes 1..n beside it
+    int match_lanes() const { return (int)lanes_.size(); }  // lanes asynchronous matches go to
+    void enter_lane(int i);
+    void leave_lane();
     void set_profiling(int level) { profiling_ = level; }
     DeviceTimers& timers() { return timers_; }
 
@@ -115,6 +126,32 @@ class Device {
     std::string info() const;
 
   private:
+    struct LaneState {
+        void* stream = nullptr;
+        uint64_t* d_ks = nullptr;
+        size_t batch_cap = 0;
+        int8_t* d_dig = nullptr;
+        size_t dig_cap = 0;
+        int* d_cmap = nullptr;
+        int* h_cmap[2] = {nullptr, nullptr};
+        void* cmap_ev[2] = {nullptr, nullptr};
+        size_t cmap_cap = 0, cmap_n = 0;
+        int cmap_stage = 0;
+        void* done_ev = nullptr;  // recorded on the lane's stream when it is left
+        bool pending = false;     // work enqueued since lane 0 last waited for it
+    };
+    std::vector<LaneState> lanes_;  // lanes 1..n
+    int lane_ = 0;                  // current lane
+    bool lanes_pending_ = false;
+    bool lanes_unsynced_ = false;   // lane work not yet host-synchronised (deferred frees)
+    void* main_ev_ = nullptr;       // lane 0's progress, waited for by a lane on entry
+    std::vector<int> deferred_free_;
+    void swap_lane(LaneState& l);
+    // the stream of the current lane; on lane 0 it first waits (device-side) for the lanes
+    void* cur_stream();
+    void join_lanes();
+    void sync_all();  // host-synchronise every lane, recycle the deferred slots
+    void free_lane(LaneState& l);
     void ensure_arena(size_t slots);
     void ensure_batch(size_t n);
     // pinned staging ring for gate descriptors: a buffer is rewritten only after

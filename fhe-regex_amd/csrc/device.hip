@@ -1209,7 +1209,7 @@ __global__ void __launch_bounds__(256) k_linear(const DevGate gg, uint64_t* __re
 }
 
 // ================================================================== host side
-#define STREAM ((hipStream_t)stream_)
+#define STREAM ((hipStream_t)cur_stream())
 
 template <int N, int K, int E>
 static void set_smem_attr() {
@@ -1301,7 +1301,14 @@ Device::Device(const Params& p, int device) : p_(p), dev_(device) {
 
 Device::~Device() {
     (void)hipSetDevice(dev_);
-    if (stream_) (void)hipStreamSynchronize(STREAM);
+    if (lane_ != 0) leave_lane();
+    for (auto& l : lanes_) {
+        if (l.stream) (void)hipStreamSynchronize((hipStream_t)l.stream);
+        free_lane(l);
+    }
+    lanes_.clear();
+    if (main_ev_) (void)hipEventDestroy((hipEvent_t)main_ev_);
+    if (stream_) (void)hipStreamSynchronize((hipStream_t)stream_);
     (void)hipFree(d_ksk_);
     (void)hipFree(d_tbsk_);
     (void)hipFree(d_kl_);
@@ -1327,7 +1334,119 @@ Device::~Device() {
     for (auto* e : event_pool_) (void)hipEventDestroy((hipEvent_t)e);
     for (auto e : ev_)
         if (e) (void)hipEventDestroy((hipEvent_t)e);
-    if (stream_) (void)hipStreamDestroy(STREAM);
+    if (stream_) (void)hipStreamDestroy((hipStream_t)stream_);
+}
+
+// ---------------------------------------------------------------- lanes
+void Device::swap_lane(LaneState& l) {
+    std::swap(stream_, l.stream);
+    std::swap(d_ks_, l.d_ks);
+    std::swap(batch_cap_, l.batch_cap);
+    std::swap(d_dig_, l.d_dig);
+    std::swap(dig_cap_, l.dig_cap);
+    std::swap(d_cmap_, l.d_cmap);
+    std::swap(h_cmap_, l.h_cmap);
+    std::swap(cmap_ev_, l.cmap_ev);
+    std::swap(cmap_cap_, l.cmap_cap);
+    std::swap(cmap_n_, l.cmap_n);
+    std::swap(cmap_stage_, l.cmap_stage);
+}
+void Device::free_lane(LaneState& l) {
+    (void)hipFree(l.d_ks);
+    (void)hipFree(l.d_dig);
+    (void)hipFree(l.d_cmap);
+    for (auto* h : l.h_cmap)
+        if (h) (void)hipHostFree(h);
+    for (auto* e : l.cmap_ev)
+        if (e) (void)hipEventDestroy((hipEvent_t)e);
+    if (l.done_ev) (void)hipEventDestroy((hipEvent_t)l.done_ev);
+    if (l.stream) (void)hipStreamDestroy((hipStream_t)l.stream);
+    l = LaneState{};
+}
+void Device::set_lanes(int n) {
+    if (n < 1 || n > 8) throw Error(FR_ERR_INVALID, "lanes: 1..8");
+    if (lane_ != 0) throw Error(FR_ERR_INVALID, "lanes: changed inside a lane");
+    sync_all();
+    // n >= 2: n lanes besides lane 0 (matches go to them only: a match on lane 0 would wait
+    // for the other lanes at its first launch)
+    const int extra = n >= 2 ? n : 0;
+    while ((int)lanes_.size() > extra) {
+        free_lane(lanes_.back());
+        lanes_.pop_back();
+    }
+    if (!main_ev_ && extra) {
+        hipEvent_t ev;
+        HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        main_ev_ = ev;
+    }
+    while ((int)lanes_.size() < extra) {
+        LaneState l;
+        hipStream_t st;
+        HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        l.stream = st;
+        for (auto*& e : l.cmap_ev) {
+            hipEvent_t ev;
+            HIP_CHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+            HIP_CHECK(hipEventRecord(ev, st));  // complete before first use
+            e = ev;
+        }
+        hipEvent_t dv;
+        HIP_CHECK(hipEventCreateWithFlags(&dv, hipEventDisableTiming));
+        l.done_ev = dv;
+        lanes_.push_back(l);
+        // the lane's keyswitch scratch at the main lane's size (ensure_batch on entry grows it)
+        const int i = (int)lanes_.size();
+        enter_lane(i);
+        ensure_batch(1024);
+        leave_lane();
+    }
+}
+void Device::enter_lane(int i) {
+    if (lane_ != 0) throw Error(FR_ERR_INVALID, "lanes: already inside a lane");
+    if (i <= 0) return;
+    if (i > (int)lanes_.size()) throw Error(FR_ERR_INVALID, "lanes: no such lane");
+    // the lane waits for lane 0's own work so far -- not for the other lanes (no join here:
+    // that would chain every lane behind the previous one); lane 0 waited for the lanes at
+    // its last operation, so their results that operation consumed are covered too
+    HIP_CHECK(hipEventRecord((hipEvent_t)main_ev_, (hipStream_t)stream_));
+    swap_lane(lanes_[i - 1]);
+    lane_ = i;
+    HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream_, (hipEvent_t)main_ev_, 0));
+}
+void Device::leave_lane() {
+    if (lane_ == 0) return;
+    LaneState& l = lanes_[lane_ - 1];
+    HIP_CHECK(hipEventRecord((hipEvent_t)l.done_ev, (hipStream_t)stream_));
+    swap_lane(l);
+    l.pending = true;
+    lanes_pending_ = true;
+    lanes_unsynced_ = true;
+    lane_ = 0;
+}
+void Device::join_lanes() {
+    if (!lanes_pending_ || lane_ != 0) return;
+    for (auto& l : lanes_)
+        if (l.pending) {
+            HIP_CHECK(hipStreamWaitEvent((hipStream_t)stream_, (hipEvent_t)l.done_ev, 0));
+            l.pending = false;
+        }
+    lanes_pending_ = false;
+}
+void* Device::cur_stream() {
+    if (lane_ == 0 && lanes_pending_) join_lanes();
+    return stream_;
+}
+void Device::sync_all() {
+    HIP_CHECK(hipStreamSynchronize((hipStream_t)stream_));
+    for (auto& l : lanes_)
+        if (l.stream) HIP_CHECK(hipStreamSynchronize((hipStream_t)l.stream));
+    if (lane_ == 0) {
+        for (auto& l : lanes_) l.pending = false;
+        lanes_pending_ = false;
+    }
+    lanes_unsynced_ = false;
+    free_slots_.insert(free_slots_.end(), deferred_free_.begin(), deferred_free_.end());
+    deferred_free_.clear();
 }
 
 std::string Device::info() const {
@@ -1347,6 +1466,7 @@ void Device::ensure_arena(size_t slots) {
     uint64_t* nb = nullptr;
     HIP_CHECK(hipMalloc(&nb, (size_t)8 * p_.slot_stride() * cap));
     if (d_arena_) {
+        sync_all();  // no launch of any lane may still use the old arena
         HIP_CHECK(hipMemcpyAsync(nb, d_arena_, (size_t)8 * p_.slot_stride() * arena_cap_, hipMemcpyDeviceToDevice, STREAM));
         HIP_CHECK(hipStreamSynchronize(STREAM));
         HIP_CHECK(hipFree(d_arena_));
@@ -1370,14 +1490,16 @@ void Device::ensure_batch(size_t n) {
     size_t cap = batch_cap_ ? batch_cap_ : 1024;
     while (cap < n) cap *= 2;
     HIP_CHECK(hipStreamSynchronize(STREAM));
-    (void)hipFree(d_gates_);
     (void)hipFree(d_ks_);
-    for (auto& h : h_stage_) {
-        if (h) (void)hipHostFree(h);
-        h = nullptr;
+    if (lane_ == 0) {  // the gate staging ring belongs to lane 0 (lanes run resident plans only)
+        (void)hipFree(d_gates_);
+        for (auto& h : h_stage_) {
+            if (h) (void)hipHostFree(h);
+            h = nullptr;
+        }
+        HIP_CHECK(hipMalloc(&d_gates_, sizeof(DevGate) * cap));
+        for (auto& h : h_stage_) HIP_CHECK(hipHostMalloc(&h, sizeof(DevGate) * cap));
     }
-    HIP_CHECK(hipMalloc(&d_gates_, sizeof(DevGate) * cap));
-    for (auto& h : h_stage_) HIP_CHECK(hipHostMalloc(&h, sizeof(DevGate) * cap));
     HIP_CHECK(hipMalloc(&d_ks_, (size_t)8 * p_.ks_stride() * cap));
     batch_cap_ = cap;
 }
@@ -1392,7 +1514,10 @@ int Device::alloc_slot() {
     return (int)next_slot_++;
 }
 void Device::free_slot(int s) {
-    if (s >= 0) free_slots_.push_back(s);
+    if (s < 0) return;
+    // a lane may still read or write it: recycled after the next host sync of every lane
+    if (lanes_unsynced_ || lane_ != 0) deferred_free_.push_back(s);
+    else free_slots_.push_back(s);
 }
 
 // packed copies between arena slots and a device buffer of the caller (the
@@ -1466,7 +1591,7 @@ void Device::write_slots(const int* slots, size_t n, const uint64_t* host) {
 void Device::read_slot(int slot, uint64_t* host) {
     HIP_CHECK(hipMemcpyAsync(host, d_arena_ + (size_t)slot * p_.slot_stride(), 8 * (size_t)p_.lwe_len(),
                              hipMemcpyDeviceToHost, STREAM));
-    HIP_CHECK(hipStreamSynchronize(STREAM));
+    sync_all();
 }
 void Device::zero_slot(int slot) {
     HIP_CHECK(hipMemsetAsync(d_arena_ + (size_t)slot * p_.slot_stride(), 0, 8 * (size_t)p_.lwe_len(), STREAM));
@@ -1664,6 +1789,7 @@ void Device::bind_content(const int* cmap, size_t n) {
 void Device::run_level(const DevGate* gates, size_t n) {
     if (!n) return;
     if (!has_keys()) throw Error(FR_ERR_NO_KEY, "server key not uploaded");
+    if (lane_ != 0) throw Error(FR_ERR_INVALID, "staged gate batches run on lane 0 only");
     validate_gates(gates, n);
     ensure_batch(n);
     // d_gates_ / d_ks_ are reused in stream order (this level's copy runs after
@@ -1780,7 +1906,7 @@ void Device::run_linear(const DevGate& g) {
 }
 
 void Device::sync() {
-    HIP_CHECK(hipStreamSynchronize(STREAM));
+    sync_all();
     resolve_timers();
 }
 

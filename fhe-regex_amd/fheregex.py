@@ -141,6 +141,7 @@ _SIGS = {
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_async": (C.c_int, [C.c_void_p, C.c_int32]),
+    "fr_set_lanes": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_plan_cache_stats": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64),
                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "fr_has_match_batch": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_size_t, C.c_char_p,
@@ -335,6 +336,11 @@ class Context:
     def set_async(self, on: bool):
         """has_match returns once its launches are enqueued (default) or blocks (False)."""
         _check(lib().fr_set_async(self.h, int(on)))
+
+    def set_lanes(self, n: int):
+        """fr_set_lanes: consecutive asynchronous matches round-robin over n streams of this
+        context (one key, a plan copy per lane); every other call waits for them device-side."""
+        _check(lib().fr_set_lanes(self.h, int(n)))
 
     def set_plan_cache_slots(self, max_slots: int):
         """Bound on the intermediate arena slots held by all cached plans."""

@@ -199,6 +199,14 @@ int fr_run_gates(fr_ctx* ctx, fr_gate* gates, size_t n);
  * work with the device's; fr_set_async(ctx, 0) makes the engine calls block until
  * the device has finished. */
 int fr_set_async(fr_ctx* ctx, int32_t on);
+/* Lanes (round 5; serving with one key): n >= 2 gives the context's device n more
+ * streams ("lanes") beside its own, each with its own keyswitch scratch and content map;
+ * consecutive asynchronous
+ * matches of a cacheable plan go round-robin over the lanes (each lane its own copy of the
+ * plan), so one match's small levels share the chip with the next match's first level.
+ * Every other operation runs on lane 0 after the lanes' enqueued work (device-side event
+ * waits); results are bit-identical to n = 1.  n = 1 (default): one stream.  1 <= n <= 8. */
+int fr_set_lanes(fr_ctx* ctx, int32_t n);
 int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, fr_ct* out,
                  fr_match_stats* stats);
 /* Same, restricted to start offsets [start_lo, start_hi) — the per-GPU shard of

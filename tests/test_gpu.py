@@ -1062,3 +1062,42 @@ def test_faithful_tree_full_metric(gctx, oracle_k1):
         gctx.set_lowering(F.LOWER_THRESHOLD)
     assert got == 1
     assert (st.pbs, st.levels) == (3047, 12)
+
+
+def test_lanes_bit_identical(gctx, key_blob):
+    """fr_set_lanes: consecutive asynchronous matches round-robin over 3 lanes (streams) of ONE
+    context with one key, each lane its own plan copy: every output word for word equal to the
+    one-lane match; an OR on lane 0 right after them (device-side join, no host wait) reads
+    finished results; released handles and slots are reused across lanes safely"""
+    p = gctx.params
+    ctx = F.Context(device=0, params=F.default_params(k=p.k, N=p.N, ring=p.ring))
+    ctx.load_client_key(key_blob)
+    ctx.gen_server_key(SEED)
+    rng = np.random.default_rng(61)
+    texts = []
+    for i in range(3):
+        t = _printable(rng, 64).replace("abc", "abd")
+        texts.append(t[:10 * i + 5] + "abc" + t[10 * i + 8:] if i != 1 else t)
+    hs = [ctx.upload_radix(ctx.encrypt_str(t, seed=80 + i)) for i, t in enumerate(texts)]
+    ref = []
+    for h in hs:
+        o, _ = ctx.has_match(h, "/abc/")
+        ref.append(ctx.download_radix(o))
+        ctx.release(o)
+    exp = [ro.has_match_reach(t, "/abc/") for t in texts]
+    assert [ctx.decrypt_radix(w) for w in ref] == exp == [1, 0, 1]
+    ctx.set_lanes(3)
+    try:
+        for rnd in range(2):  # the second round reuses the first round's released slots
+            outs = [ctx.has_match(hs[i % 3], "/abc/")[0] for i in range(7)]
+            both = ctx.or_many([outs[1], outs[2]])  # lane 0, after the lanes' work
+            for i, o in enumerate(outs):
+                assert np.array_equal(ctx.download_radix(o), ref[i % 3]), (rnd, i)
+            assert ctx.decrypt_radix(ctx.download_radix(both)) == 1
+            for o in outs + [both]:
+                ctx.release(o)
+    finally:
+        ctx.set_lanes(1)
+    o, _ = ctx.has_match(hs[0], "/abc/")
+    assert np.array_equal(ctx.download_radix(o), ref[0])
+    ctx.close()

@@ -50,6 +50,17 @@ def test_set_profiling_rejects_invalid_levels():
         ctx.set_profiling(1)
 
 
+def test_set_lanes_validates():
+    """fr_set_lanes takes 1..8 lanes and needs the device (host-only context: NoDevice)"""
+    ctx = F.Context(device=-1)
+    for bad in (0, -1, 9):
+        with pytest.raises(F.FheRegexError) as e:
+            ctx.set_lanes(bad)
+        assert not isinstance(e.value, F.NoDevice)
+    with pytest.raises(F.NoDevice):
+        ctx.set_lanes(2)
+
+
 @pytest.mark.parametrize("v", load("parser_vectors.json"), ids=lambda v: v["pattern"])
 def test_parser_golden(v):
     assert F.parse(v["pattern"]) == v["ast"]
