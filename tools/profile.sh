@@ -10,7 +10,7 @@ out=${1:-gpurun_out/prof}
 shift
 mkdir -p "$out"
 export TMPDIR=/tmp
-B="bench.py --steps 5 --warmup 2 --cpu-sample 0 --probe= --fresh-steps 0 --faithful-steps 0 --inflight 0 $*"
+B="bench.py --steps 5 --warmup 2 --cpu-sample 0 --probe= --fresh-steps 0 --faithful-steps 0 --faithful-tree-steps 0 --inflight 0 --lanes 0 $*"
 step() { local t=$1; shift; echo "== $*" >&2; timeout -k 10 "$t" "$@" || { echo "step failed rc=$?"; exit 1; }; }
 step 400 rocprofv3 --kernel-trace --stats -d "$out/trace" -o run --output-format csv -- python3 $B > "$out/trace.log" 2>&1
 step 400 rocprofv3 --pmc FETCH_SIZE -d "$out/pmc_fetch" -o run --output-format csv -- python3 $B > "$out/pmc_fetch.log" 2>&1
