@@ -1516,8 +1516,13 @@ int Device::alloc_slot() {
 void Device::free_slot(int s) {
     if (s < 0) return;
     // a lane may still read or write it: recycled after the next host sync of every lane
-    if (lanes_unsynced_ || lane_ != 0) deferred_free_.push_back(s);
-    else free_slots_.push_back(s);
+    if (lanes_unsynced_ || lane_ != 0) {
+        deferred_free_.push_back(s);
+        // a serving loop that never downloads: recycle in bulk rather than grow the arena
+        if (deferred_free_.size() >= (size_t)1 << 16) sync_all();
+    } else {
+        free_slots_.push_back(s);
+    }
 }
 
 // packed copies between arena slots and a device buffer of the caller (the

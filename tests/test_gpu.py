@@ -1096,6 +1096,13 @@ def test_lanes_bit_identical(gctx, key_blob):
             assert ctx.decrypt_radix(ctx.download_radix(both)) == 1
             for o in outs + [both]:
                 ctx.release(o)
+        # batched and ranged matches go to the lanes too (their own plans), still exact
+        bo, _ = ctx.has_match_batch([hs[0], hs[2]], "/abc/")
+        ro_, _ = ctx.has_match(hs[2], "/abc/", 0, 40)
+        assert [np.array_equal(ctx.download_radix(b), ref[i]) for b, i in zip(bo, (0, 2))] == [True, True]
+        assert ctx.decrypt_radix(ctx.download_radix(ro_)) == int("abc" in texts[2][:42])
+        for h in list(bo) + [ro_]:
+            ctx.release(h)
     finally:
         ctx.set_lanes(1)
     o, _ = ctx.has_match(hs[0], "/abc/")
