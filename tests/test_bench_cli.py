@@ -130,3 +130,22 @@ def test_one_rank_rccl_group_pipeline():
     assert d["n_gpus"] == 1 and d["config"]["shard"] == "starts" and "RCCL" in d["config"]["parallelism"]
     assert d["results_ok_steps"] is True and d["result_decrypted"] == d["result_expected"] == [1]
     assert len(d["per_rank"]) == 1 and d["weak_matches"]["results_ok_ranks"] == 1
+
+
+@pytest.mark.gpu
+def test_two_gloo_ranks_config4_named_length():
+    """BASELINE config 4 at N = 2 (two gloo ranks sharing the box's GPU): `value` is measured on
+    the named 1,024 characters split by start offsets (strong scaling), one JSON line, every
+    step's OR decrypting to the expected bit, both ranks reporting"""
+    res = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--workload", "config4",
+                          "--steps", "2", "--warmup", "1", "--weak-matches-steps", "0", "--probe=", "--saturate", "0",
+                          "--job-timeout", "280"], capture_output=True, text=True, timeout=300, env=_env())
+    assert res.returncode == 0, res.stderr[-3000:]
+    lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, res.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["content_chars"] == 1024 and d["scaling"] == "strong"
+    assert d["config"]["shard"] == "starts" and d["results_ok_steps"] is True
+    assert d["result_decrypted"] == d["result_expected"] == [1]
+    assert len(d["per_rank"]) == 2 and d["strong_starts"] == {"same_as_value": True,
+                                                              "note": d["strong_starts"]["note"]}

@@ -1108,3 +1108,25 @@ def test_lanes_bit_identical(gctx, key_blob):
     o, _ = ctx.has_match(hs[0], "/abc/")
     assert np.array_equal(ctx.download_radix(o), ref[0])
     ctx.close()
+
+
+@pytest.mark.parametrize("case,words", [(3, True), (11, True), (17, True), (8, False), (14, False), (19, False)])
+def test_faithful_tree_fuzz_scale(gctx, oracle_k1, case, words):
+    """FR_LOWER_FAITHFUL_TREE on fuzz_scale.json patterns (914-4,857 rotations, 11-19 levels
+    where the serial fold takes 133-764): word for word against the oracle's evaluation of the
+    same schedule (the smaller ones), else the decrypted bit against the position-set simulator"""
+    cse = load("fuzz_scale.json")["cases"][case]
+    gctx.set_lowering(F.LOWER_FAITHFUL_TREE)
+    try:
+        if words:
+            got = _match_words_vs_oracle(gctx, oracle_k1, cse["content"], cse["pattern"], 5000 + case,
+                                         lowering=F.LOWER_FAITHFUL_TREE)
+        else:
+            hs = gctx.upload_radix(gctx.encrypt_str(cse["content"], seed=5000 + case))
+            out, _ = gctx.has_match(hs, cse["pattern"])
+            got = gctx.decrypt_radix(gctx.download_radix(out))
+            for h in hs + [out]:
+                gctx.release(h)
+    finally:
+        gctx.set_lowering(F.LOWER_THRESHOLD)
+    assert got == cse["expected"]
