@@ -1293,7 +1293,16 @@ int fr_set_plan_cache(fr_ctx* ctx, size_t capacity) {
 int fr_set_lanes(fr_ctx* ctx, int32_t n) {
     FR_TRY({
         NEED(ctx && n >= 1 && n <= 8);
-        ctx->device().set_lanes(n);
+        Device& dev = ctx->device();
+        if (n == 1 ? dev.match_lanes() == 0 : dev.match_lanes() == n) return FR_OK;
+        // the lanes' plan copies go with the lanes (their slots are held by the cache)
+        fr_plan_cache& pc = *ctx->plans;
+        for (size_t i = pc.entries.size(); i-- > 0;)
+            if (pc.entries[i]->key.find("|lane") != std::string::npos) {
+                drop_cached(ctx, *pc.entries[i]);
+                pc.entries.erase(pc.entries.begin() + (long)i);
+            }
+        dev.set_lanes(n);
         ctx->next_lane = 0;
     })
 }
