@@ -442,6 +442,9 @@ def main():
     ap.add_argument("--lanes", type=int, default=4,
                     help="N=1: secondary record of matches in flight on the lanes (streams) of ONE context with one "
                          "key (fr_set_lanes; 0: skip)")
+    ap.add_argument("--start-parts", type=int, default=0, choices=range(0, 17), metavar="{0..16}",
+                    help="start shards: booleans per rank per match (fr_has_match_parts); 0: 16 // world (1 = "
+                         "one boolean per rank, an extra OR level)")
     ap.add_argument("--faithful-steps", type=int, default=1,
                     help="N=1 metric: timed matches of the reference-structured lowering (FR_LOWER_FAITHFUL) "
                          "for the `faithful` sub-record (0: skip)")
@@ -659,10 +662,16 @@ def main():
         return {"handles": np.asarray(hs, dtype=np.uint32), "lo": jlo, "hi": jhi, "L": Lj, "expected": exp,
                 "window": (jwlo, jwhi)}
 
+    # parts per rank (fr_has_match_parts): each rank's OR tree stops at <= P booleans, so the
+    # world * P gathered booleans are ONE threshold OR: the tree's last level runs once, on
+    # rank 0, instead of once per rank plus once to combine (/abc/ on 256 chars at N = 2..8:
+    # 4 levels, as at N = 1, instead of 5)
+    P = args.start_parts or (max(1, 16 // world) if world <= 16 else 1)
+
     def starts_pipeline(n, times=None, job=None):
         """n start-sharded matches (north_star's per-start-offset variants + final bitor,
-        engine.rs:15-35): per step every rank enqueues its start range's match, exports its
-        boolean device to device into that step's row (stream-ordered) and all-gathers the
+        engine.rs:15-35): per step every rank enqueues its start range's match as <= P
+        parts, exports them device to device into that step's row (stream-ordered) and all-gathers the
         row (RCCL on torch's stream, ordered after the export by an event on the library's
         stream; the host never waits between matches).  Rank 0 then ORs every step's
         gathered booleans in ONE launch (n independent threshold ORs).  gloo (a rehearsal:
@@ -672,22 +681,28 @@ def main():
         jh, jlo, jhi = (handles_np, lo, hi) if job is None else (job["handles"], job["lo"], job["hi"])
         # every row is overwritten by an export on the library's stream, which must not
         # overtake the allocation's work on torch's stream
-        send = torch.empty((n, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
-        recv = torch.empty((n, world, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        send = torch.empty((n, P, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
+        recv = torch.empty((n, world, P, ctx.lwe_len), dtype=torch.int64, device=f"cuda:{device}")
         lib_stream.wait_stream(torch.cuda.current_stream())
         rot, st = 0, None
         for i in range(n):
             t = time.perf_counter()
-            out, st = ctx.has_match(jh, pattern, jlo, jhi)
+            if P > 1:  # up to P parts; a short list repeats its first (OR is idempotent)
+                outs_i, st = ctx.has_match_parts(jh, pattern, jlo, jhi, P)
+                outs_i += [outs_i[0]] * (P - len(outs_i))
+            else:
+                out, st = ctx.has_match(jh, pattern, jlo, jhi)
+                outs_i = [out]
             rot += st.blind_rotations
             if rccl:
-                ctx.export_bool_device_async([out], send[i].data_ptr())
+                ctx.export_bool_device_async(outs_i, send[i].data_ptr())
                 ev = torch.cuda.Event()
                 ev.record(lib_stream)
                 torch.cuda.current_stream().wait_event(ev)
             else:
-                ctx.export_bool_device([out], send[i].data_ptr())
-            ctx.release(out)  # stream-ordered: a later user of its slot runs after the export
+                ctx.export_bool_device(outs_i, send[i].data_ptr())
+            for h in set(outs_i):
+                ctx.release(h)  # stream-ordered: a later user of its slot runs after the export
             t2 = time.perf_counter()
             if rccl:
                 dist.all_gather_into_tensor(recv[i].view(-1), send[i])
@@ -701,12 +716,13 @@ def main():
         if rank != 0:
             return [], rot, st
         t = time.perf_counter()
-        parts = ctx.import_bool_device(recv.data_ptr(), n * world)
-        if world <= 16:
-            res = ctx.or_each([parts[i * world:(i + 1) * world] for i in range(n)])
+        parts = ctx.import_bool_device(recv.data_ptr(), n * world * P)
+        g = world * P  # booleans per step
+        if g <= 16:
+            res = ctx.or_each([parts[i * g:(i + 1) * g] for i in range(n)])
             rot += n
         else:
-            res = [ctx.or_many(parts[i * world:(i + 1) * world]) for i in range(n)]
+            res = [ctx.or_many(parts[i * g:(i + 1) * g]) for i in range(n)]
             rot += 2 * n
         for h in parts:
             ctx.release(h)
@@ -886,7 +902,7 @@ def main():
             s_per_rank.append(d)
         strong_starts = {"value": float(sm[0]) / float(mx[0]), "unit": "gate-bootstraps/s",
                          "ms_per_step": float(mx[0]) * 1e3 / ss_steps, "steps": ss_steps,
-                         "content_chars": job["L"], "scaling": "strong",
+                         "content_chars": job["L"], "scaling": "strong", "parts_per_rank": P,
                          "workload": f"{pattern} on {job['L']} chars (the workload's named length) split by start "
                                      f"offsets over {world} ranks, {coll_name} gather, OR on rank 0",
                          "results_ok_steps": bool(sm[1] >= world), "result_expected": job["expected"],
@@ -1125,7 +1141,8 @@ def main():
         "data": "synthetic: seeded content, real encryptions under the reference fixture client key",
         "config": {"workload": work, "content_chars": L, "matches_per_gpu": M, "params": args.params,
                    "ring": ring_name, "lowering": args.lowering, "engine": args.engine, "content": kind,
-                   "scaling": "strong" if strong else "weak", "shard": shard, "parallelism": par},
+                   "scaling": "strong" if strong else "weak", "shard": shard, "parallelism": par,
+                   "start_parts": P if starts else None},
         "match_ms": ms_per_step,
         "blind_rotations_per_step": total_rot / args.steps,
         "lut_outputs_per_match": float(st.pbs) / (M if shard == "matches" else 1),

@@ -402,7 +402,7 @@ struct CachedMatch {
     std::vector<int32_t> sig;  // canonical content shape (content_signature)
     Plan plan;
     size_t n_gates = 0;        // program gates of one match (copy m's gates start at m * n_gates)
-    int32_t out_gate = -1, out_w = 0, out_const = 0;
+    std::vector<ProgOut> outs;  // one match's outputs (its parts, fr_has_match_parts)
     uint64_t ct_ops = 0, cache_hits = 0, n_branches = 0;
     uint64_t last_use = 0;
 };
@@ -519,8 +519,10 @@ static void evict_for(fr_ctx* ctx, size_t entries, size_t slots) {
 // M independent matches of one pattern over M contents of n positions each
 // (content[m * n + q]): one plan whose program is M copies of the match's lowered
 // program, so every level of the M matches shares its launches (M = 1: has_match).
+// parts > 1 (fr_has_match_parts): each match returns up to `parts` booleans whose OR is
+// its result, outs[m * P + j] with P = *n_parts (the same for every m).
 static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, const char* pattern, size_t lo,
-                       size_t hi, fr_ct* outs, fr_match_stats* st) {
+                       size_t hi, fr_ct* outs, fr_match_stats* st, size_t parts = 1, size_t* n_parts = nullptr) {
     double t0 = now_ms();
     pattern = pattern ? pattern : "";
     Device& dev = ctx->device();
@@ -547,6 +549,7 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
     } lane_scope{dev};
     if (pc.capacity) {
         key = match_key(ctx, pattern, n, M, lo, hi);
+        if (parts > 1) key += "|parts" + std::to_string(parts);
         if (lane) key += "|lane" + std::to_string(lane);
         sig = content_signature(ctx, content, n * M, &cmap);
         for (auto& e : pc.entries)
@@ -568,17 +571,21 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
         rec.ct_ops = hit->ct_ops;
         rec.cache_hits = hit->cache_hits;
         rec.n_branches = hit->n_branches;
-        for (size_t m = 0; m < M; ++m) {
-            const int og = hit->out_gate < 0 ? -1 : hit->out_gate + (int)(m * hit->n_gates);
-            outs[m] = make_output(ctx, og, hit->out_w, hit->out_const, hit->plan.slot, false);
-        }
+        const size_t nO = hit->outs.size();
+        for (size_t m = 0; m < M; ++m)
+            for (size_t j = 0; j < nO; ++j) {
+                const ProgOut& o = hit->outs[j];
+                const int og = o.gate < 0 ? -1 : o.gate + (int)(m * hit->n_gates);
+                outs[m * nO + j] = make_output(ctx, og, o.w, o.cst, hit->plan.slot, false);
+            }
+        if (n_parts) *n_parts = nO;
         if (!ctx->async_match) dev.sync();
     } else {
         ++pc.misses;
         ValueDag dag;
         GrammarScope grammar(ctx->grammar);
         rec = record_has_match_engine(dag, n, pattern, lo, hi, ctx->engine);
-        Program prog = lower(dag, rec.root, ctx->lowering);
+        Program prog = lower(dag, rec.root, ctx->lowering, (int)parts);
         // validate the referenced content handles of every match
         for (auto& g : prog.gates)
             for (auto& in : g.ins)
@@ -605,16 +612,18 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
         if (keep) evict_for(ctx, 1, G * M);  // before the new plan allocates its slots
         Plan P = compile_plan(ctx, gates, inputs, keep);
         add_plan_stats(P, &local);
-        auto out_of = [&](size_t m) { return prog.out_gate < 0 ? -1 : prog.out_gate + (int)(m * G); };
+        const size_t nO = prog.outs.size();
+        if (n_parts) *n_parts = nO;
+        auto out_of = [&](size_t m, size_t j) {
+            return prog.outs[j].gate < 0 ? -1 : prog.outs[j].gate + (int)(m * G);
+        };
         if (keep) {
             // keep the plan: its slots stay allocated, its batches go to the device once
             auto e = std::make_unique<CachedMatch>();
             e->key = std::move(key);
             e->sig = std::move(sig);
             e->n_gates = G;
-            e->out_gate = prog.out_gate;
-            e->out_w = prog.out_w;
-            e->out_const = prog.out_const;
+            e->outs = prog.outs;
             e->ct_ops = rec.ct_ops;
             e->cache_hits = rec.cache_hits;
             e->n_branches = rec.n_branches;
@@ -628,11 +637,16 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
             dev.bind_content(cmap.data(), cmap.size());
             t1 = now_ms();
             launch_plan(dev, c.plan);
-            for (size_t m = 0; m < M; ++m) outs[m] = make_output(ctx, out_of(m), c.out_w, c.out_const, c.plan.slot, false);
+            for (size_t m = 0; m < M; ++m)
+                for (size_t j = 0; j < nO; ++j)
+                    outs[m * nO + j] = make_output(ctx, out_of(m, j), prog.outs[j].w, prog.outs[j].cst, c.plan.slot, false);
         } else {
             t1 = now_ms();
             launch_plan(dev, P);
-            for (size_t m = 0; m < M; ++m) outs[m] = make_output(ctx, out_of(m), prog.out_w, prog.out_const, P.slot, true);
+            // one output takes its gate's slot; parts get copies (two parts may read one gate)
+            for (size_t m = 0; m < M; ++m)
+                for (size_t j = 0; j < nO; ++j)
+                    outs[m * nO + j] = make_output(ctx, out_of(m, j), prog.outs[j].w, prog.outs[j].cst, P.slot, nO == 1);
             free_plan_slots(dev, P.slot);  // later users of these slots are ordered after the launches (one stream)
         }
         if (!ctx->async_match) dev.sync();
@@ -1349,6 +1363,44 @@ int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n, const char* 
     })
 }
 
+int fr_has_match_parts(fr_ctx* ctx, const fr_ct* content, size_t n, const char* pattern, size_t lo, size_t hi,
+                       size_t max_parts, fr_ct* out, size_t* n_parts, fr_match_stats* st) {
+    FR_TRY({
+        NEED(ctx && out && n_parts && pattern && (content || !n) && lo <= hi);
+        NEED(max_parts >= 1 && max_parts <= (size_t)MAX_FANIN);
+        match_impl(ctx, content, n, 1, pattern, lo, hi, out, st, max_parts, n_parts);
+    })
+}
+
+int fr_plain_match_parts(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                         int32_t engine, int32_t grammar, size_t max_parts, fr_plain_result* out, int32_t* parts,
+                         size_t* n_parts) {
+    FR_TRY({
+        NEED((content || !len) && pattern && out && parts && n_parts && lo <= hi);
+        NEED(max_parts >= 1 && max_parts <= (size_t)MAX_FANIN);
+        NEED(lowering >= FR_LOWER_FAITHFUL && lowering <= FR_LOWER_FAITHFUL_TREE);
+        NEED(engine >= FR_ENGINE_AUTO && engine <= FR_ENGINE_MERGED);
+        NEED(grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT);
+        ValueDag dag;
+        GrammarScope scope(grammar);
+        Recorded rec = record_has_match_engine(dag, len, pattern, lo, hi, engine);
+        std::vector<int16_t> memo;
+        std::memset(out, 0, sizeof *out);
+        out->ct_ops = rec.ct_ops;
+        out->cache_hits = rec.cache_hits;
+        out->n_branches = rec.n_branches;
+        out->result_recorded = dag.eval(rec.root, (const uint8_t*)content, memo);
+        Program prog = lower(dag, rec.root, lowering, (int)max_parts);
+        out->pbs = prog.gates.size();
+        out->levels = (uint64_t)prog.levels;
+        out->max_level_width = prog.max_width;
+        std::vector<int> vals;
+        out->result_lowered = eval_program_parts(prog, (const uint8_t*)content, len, vals);
+        for (size_t j = 0; j < vals.size(); ++j) parts[j] = vals[j];
+        *n_parts = vals.size();
+    })
+}
+
 int fr_parse(const char* pattern, char* buf, size_t len) {
     return fr_parse_ex(pattern, FR_GRAMMAR_REFERENCE, buf, len);
 }
@@ -1625,21 +1677,34 @@ int fr_shard_free(fr_ctx* ctx, fr_shard* sh) {
 int fr_schedule_match(size_t n_chars, const char* pattern, size_t lo, size_t hi, int32_t lowering, int32_t engine,
                       int32_t grammar, int32_t multi_value, fr_job* jobs, size_t jobs_cap, size_t* n_jobs,
                       uint32_t* level_off, size_t level_cap, size_t* n_levels, int32_t* out3) {
+    size_t n_parts = 0;
+    return fr_schedule_match_parts(n_chars, pattern, lo, hi, lowering, engine, grammar, multi_value, 1, jobs, jobs_cap,
+                                   n_jobs, level_off, level_cap, n_levels, out3, &n_parts);
+}
+
+int fr_schedule_match_parts(size_t n_chars, const char* pattern, size_t lo, size_t hi, int32_t lowering,
+                            int32_t engine, int32_t grammar, int32_t multi_value, size_t max_parts, fr_job* jobs,
+                            size_t jobs_cap, size_t* n_jobs, uint32_t* level_off, size_t level_cap, size_t* n_levels,
+                            int32_t* outs3, size_t* n_parts) {
     FR_TRY({
-        NEED(pattern && n_jobs && n_levels && out3 && lo <= hi);
+        NEED(pattern && n_jobs && n_levels && outs3 && n_parts && lo <= hi);
+        NEED(max_parts >= 1 && max_parts <= (size_t)MAX_FANIN);
         ValueDag dag;
         GrammarScope gs(grammar);
         Recorded rec = record_has_match_engine(dag, n_chars, pattern, lo, hi, engine);
-        Program prog = lower(dag, rec.root, lowering);
+        Program prog = lower(dag, rec.root, lowering, (int)max_parts);
         Schedule S = build_schedule(prog.gates, n_chars, multi_value != 0, [](int cb, int& key, int&) {
             key = cb;
             return true;
         });
         *n_jobs = S.jobs.size();
         *n_levels = S.level_off.size() - 1;
-        out3[0] = prog.out_gate;
-        out3[1] = prog.out_w;
-        out3[2] = prog.out_const;
+        *n_parts = prog.outs.size();
+        for (size_t j = 0; j < prog.outs.size(); ++j) {
+            outs3[3 * j] = prog.outs[j].gate;
+            outs3[3 * j + 1] = prog.outs[j].w;
+            outs3[3 * j + 2] = prog.outs[j].cst;
+        }
         if (jobs) {
             NEED(jobs_cap >= S.jobs.size());
             static_assert(sizeof(fr_job) == sizeof(DevGate), "fr_job mirrors DevGate");

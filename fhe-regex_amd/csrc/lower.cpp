@@ -246,8 +246,13 @@ struct Lowerer {
         if (f.k == Form::LIT) return f.lit;
         if (f.k == Form::CONST) throw Error(FR_ERR_INVALID, "lowering: cannot materialize a constant");
         bool is_and = f.k == Form::AND;
-        std::vector<Lit> lits = f.lits;
-        while ((int)lits.size() > MAX_FANIN) {
+        std::vector<Lit> lits = reduce(is_and, f.lits, MAX_FANIN);
+        if (lits.size() == 1) return lits[0];
+        return Lit{threshold_gate(is_and, lits), false};
+    }
+    // levels of threshold gates (fan-in <= 16, balanced chunks) until <= keep literals remain
+    std::vector<Lit> reduce(bool is_and, std::vector<Lit> lits, size_t keep) {
+        while (lits.size() > keep) {
             size_t m = lits.size();
             size_t chunks = (m + MAX_FANIN - 1) / MAX_FANIN;
             std::vector<Lit> next;
@@ -260,8 +265,13 @@ struct Lowerer {
             }
             lits = std::move(next);
         }
-        if (lits.size() == 1) return lits[0];
-        return Lit{threshold_gate(is_and, lits), false};
+        return lits;
+    }
+    // the parts of a root: an OR form's literals reduced to <= max_parts, else one literal
+    std::vector<Lit> parts(const Form& f0, size_t max_parts) {
+        if (f0.k == Form::SET) return parts(expand_set(f0), max_parts);
+        if (f0.k == Form::OR && max_parts > 1) return reduce(false, f0.lits, max_parts);
+        return {materialize(f0)};
     }
     static Form lit_form(Lit l) {
         Form f;
@@ -636,25 +646,23 @@ void compute_levels(Program& prog) {
     for (auto w : width) prog.max_width = std::max(prog.max_width, w);
 }
 
-Program lower(const ValueDag& dag, int root, int mode) {
+Program lower(const ValueDag& dag, int root, int mode, int max_parts) {
+    if (max_parts < 1 || max_parts > MAX_FANIN) throw Error(FR_ERR_INVALID, "lowering: parts must be in [1, 16]");
     Lowerer lw(dag, mode);
     Form f = mode == FR_LOWER_FAITHFUL ? lw.lower_f(root)
              : mode == FR_LOWER_FAITHFUL_TREE ? lw.lower_ft(root) : lw.lower_t(root);
-    if (f.k == Form::CONST) {
-        lw.prog.out_gate = -1;
-        lw.prog.out_const = f.c;
-        lw.prog.out_w = 0;
-    } else {
-        Lit l = lw.materialize(f);
-        lw.prog.out_gate = l.gate;
-        lw.prog.out_const = l.neg ? 1 : 0;
-        lw.prog.out_w = l.neg ? -1 : 1;
-    }
-    // drop gates not reachable from the output (e.g. materialized then merged)
     Program& p = lw.prog;
+    if (f.k == Form::CONST) {
+        p.outs.push_back(ProgOut{-1, 0, f.c});
+    } else {
+        for (const Lit& l : lw.parts(f, (size_t)max_parts))
+            p.outs.push_back(ProgOut{l.gate, l.neg ? -1 : 1, l.neg ? 1 : 0});
+    }
+    // drop gates not reachable from the outputs (e.g. materialized then merged)
     std::vector<char> live(p.gates.size(), 0);
-    if (p.out_gate >= 0) {
-        std::vector<int> st{p.out_gate};
+    for (const ProgOut& o : p.outs) {
+        if (o.gate < 0) continue;
+        std::vector<int> st{o.gate};
         while (!st.empty()) {
             int g = st.back();
             st.pop_back();
@@ -674,14 +682,23 @@ Program lower(const ValueDag& dag, int root, int mode) {
         remap[g] = (int)out.gates.size();
         out.gates.push_back(std::move(ng));
     }
-    out.out_gate = p.out_gate >= 0 ? remap[p.out_gate] : -1;
-    out.out_const = p.out_const;
-    out.out_w = p.out_w;
+    for (ProgOut o : p.outs) {
+        if (o.gate >= 0) o.gate = remap[o.gate];
+        out.outs.push_back(o);
+    }
+    out.out_gate = out.outs[0].gate;
+    out.out_w = out.outs[0].w;
+    out.out_const = out.outs[0].cst;
     compute_levels(out);
     return out;
 }
 
 int eval_program(const Program& prog, const uint8_t* content, size_t L) {
+    std::vector<int> parts;
+    return eval_program_parts(prog, content, L, parts);
+}
+
+int eval_program_parts(const Program& prog, const uint8_t* content, size_t L, std::vector<int>& parts) {
     std::vector<int> val(prog.gates.size(), 0);
     for (size_t g = 0; g < prog.gates.size(); ++g) {
         const PGate& G = prog.gates[g];
@@ -706,8 +723,17 @@ int eval_program(const Program& prog, const uint8_t* content, size_t L) {
             val[g] = G.lut[s / 2];
         }
     }
-    if (prog.out_gate < 0) return prog.out_const;
-    return prog.out_const + prog.out_w * val[prog.out_gate];
+    parts.clear();
+    if (prog.outs.size() > 1) {
+        int any = 0;
+        for (const ProgOut& o : prog.outs) {
+            parts.push_back(o.gate < 0 ? o.cst : o.cst + o.w * val[o.gate]);
+            any |= parts.back();
+        }
+        return any;
+    }
+    parts.push_back(prog.out_gate < 0 ? prog.out_const : prog.out_const + prog.out_w * val[prog.out_gate]);
+    return parts[0];
 }
 
 }  // namespace fr

@@ -38,20 +38,33 @@ struct PGate {
     uint8_t lut[16] = {0};
     int32_t level = 0;
 };
+// one boolean output: cst + w * gates[gate]   (gate == -1: the constant cst)
+struct ProgOut {
+    int32_t gate = -1, w = 0, cst = 0;
+};
 struct Program {
     std::vector<PGate> gates;
     // result = out_const + out_w * gates[out_gate]   (out_gate == -1: constant)
     int32_t out_gate = -1, out_const = 0, out_w = 0;
+    // the outputs: {out_*} alone, or (lower's max_parts > 1) up to max_parts booleans
+    // whose OR is the result
+    std::vector<ProgOut> outs;
     int32_t levels = 0;
     size_t max_width = 0;
 };
 
 constexpr int MAX_FANIN = 16;
 
-Program lower(const ValueDag& dag, int root, int mode);
+// max_parts > 1: a root OR (the has_match fold over start offsets, engine.rs:22-35)
+// stops its threshold tree at <= max_parts literals and outputs them as parts, so the
+// caller's own OR of several parts lists (start shards on several GPUs) is the
+// tree's last level instead of one more.  Faithful lowerings and non-OR roots: one part.
+Program lower(const ValueDag& dag, int root, int mode, int max_parts = 1);
 // Plaintext semantics of a program (LUT semantics, with the [0,16) range
-// check); returns the result value.
+// check); returns the result value (several parts: their OR).
 int eval_program(const Program& prog, const uint8_t* content, size_t L);
+// the same, and each output's value in `parts`
+int eval_program_parts(const Program& prog, const uint8_t* content, size_t L, std::vector<int>& parts);
 void compute_levels(Program& prog);
 
 // LUT builders

@@ -137,6 +137,16 @@ _SIGS = {
                                C.POINTER(MatchStats)]),
     "fr_has_match_range": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t,
                                      C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(MatchStats)]),
+    "fr_has_match_parts": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.c_size_t, C.c_char_p, C.c_size_t,
+                                     C.c_size_t, C.c_size_t, C.POINTER(C.c_uint32), C.POINTER(C.c_size_t),
+                                     C.POINTER(MatchStats)]),
+    "fr_plain_match_parts": (C.c_int, [C.c_char_p, C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32,
+                                       C.c_int32, C.c_int32, C.c_size_t, C.POINTER(PlainResult),
+                                       C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]),
+    "fr_schedule_match_parts": (C.c_int, [C.c_size_t, C.c_char_p, C.c_size_t, C.c_size_t, C.c_int32, C.c_int32,
+                                          C.c_int32, C.c_int32, C.c_size_t, C.POINTER(FrJob), C.c_size_t,
+                                          C.POINTER(C.c_size_t), C.POINTER(C.c_uint32), C.c_size_t,
+                                          C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
@@ -262,6 +272,21 @@ def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESH
     _check(lib().fr_plain_match_g(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, engine,
                                   grammar, C.byref(r)))
     return r
+
+
+def plain_match_parts(content: bytes | str, pattern: str, start_lo: int, start_hi: int, max_parts: int,
+                      lowering: int = LOWER_THRESHOLD, engine: int = ENGINE_ENUMERATE,
+                      grammar: int = GRAMMAR_REFERENCE):
+    """Host-only run of fr_has_match_parts' program: (PlainResult with result_lowered =
+    the OR of the parts, [plaintext value of each part])"""
+    if isinstance(content, str):
+        content = content.encode("latin-1")
+    r = PlainResult()
+    vals = (C.c_int32 * max_parts)()
+    n = C.c_size_t()
+    _check(lib().fr_plain_match_parts(content, len(content), pattern.encode("latin-1"), start_lo, start_hi, lowering,
+                                      engine, grammar, max_parts, C.byref(r), vals, C.byref(n)))
+    return r, list(vals)[:n.value]
 
 
 class Context:
@@ -492,6 +517,18 @@ class Context:
             _check(lib().fr_has_match_range(self.h, arr, len(content), pattern.encode("latin-1"), lo, hi,
                                             C.byref(out), C.byref(st)))
         return out.value, st
+
+    def has_match_parts(self, content: Sequence[int], pattern: str, start_lo: int, start_hi: int, max_parts: int):
+        """fr_has_match_parts: ([<= max_parts boolean handles whose OR is the range's
+        match], stats) -- a start shard's result for a caller-side OR over shards"""
+        content = np.ascontiguousarray(content, dtype=np.uint32)
+        arr = content.ctypes.data_as(C.POINTER(C.c_uint32))
+        out = (C.c_uint32 * max_parts)()
+        n = C.c_size_t()
+        st = MatchStats()
+        _check(lib().fr_has_match_parts(self.h, arr, len(content), pattern.encode("latin-1"), start_lo, start_hi,
+                                        max_parts, out, C.byref(n), C.byref(st)))
+        return list(out)[:n.value], st
 
     def has_match_batch(self, contents: Sequence[Sequence[int]], pattern: str):
         """M independent matches of one pattern over M equal-length contents in
@@ -900,22 +937,26 @@ class Schedule:
     out_w: int
     out_const: int
     n_gates: int
+    parts: List[Tuple[int, int, int]] = None  # (out_gate, out_w, out_const) of each part
 
 
 def schedule_match(n_chars: int, pattern: str, start_lo: int = 0, start_hi: Optional[int] = None,
                    lowering: int = LOWER_THRESHOLD, engine: int = ENGINE_AUTO, grammar: int = GRAMMAR_REFERENCE,
-                   multi_value: bool = True) -> Schedule:
+                   multi_value: bool = True, max_parts: int = 1) -> Schedule:
+    """max_parts > 1: fr_has_match_parts' schedule (Schedule.parts; out_* = part 0)"""
     hi = n_chars if start_hi is None else start_hi
-    nj, nl = C.c_size_t(), C.c_size_t()
-    out3 = (C.c_int32 * 3)()
+    nj, nl, npart = C.c_size_t(), C.c_size_t(), C.c_size_t()
+    outs3 = (C.c_int32 * (3 * max_parts))()
     pat = pattern.encode("latin-1")
-    args = (n_chars, pat, start_lo, hi, lowering, engine, grammar, int(multi_value))
-    _check(lib().fr_schedule_match(*args, None, 0, C.byref(nj), None, 0, C.byref(nl), out3))
+    args = (n_chars, pat, start_lo, hi, lowering, engine, grammar, int(multi_value), max_parts)
+    _check(lib().fr_schedule_match_parts(*args, None, 0, C.byref(nj), None, 0, C.byref(nl), outs3, C.byref(npart)))
     jobs = (FrJob * max(nj.value, 1))()
     off = (C.c_uint32 * (nl.value + 1))()
-    _check(lib().fr_schedule_match(*args, jobs, len(jobs), C.byref(nj), off, len(off), C.byref(nl), out3))
+    _check(lib().fr_schedule_match_parts(*args, jobs, len(jobs), C.byref(nj), off, len(off), C.byref(nl), outs3,
+                                         C.byref(npart)))
     n_gates = 1 + max([max(j.out_gate[f] for f in range(j.n_out)) for j in jobs[:nj.value]] or [-1])
-    return Schedule(list(jobs[:nj.value]), list(off), out3[0], out3[1], out3[2], n_gates)
+    parts = [(outs3[3 * j], outs3[3 * j + 1], outs3[3 * j + 2]) for j in range(npart.value)]
+    return Schedule(list(jobs[:nj.value]), list(off), parts[0][0], parts[0][1], parts[0][2], n_gates, parts)
 
 
 def content_window(n_chars: int, pattern: str, start_lo: int, start_hi: int, lowering: int = LOWER_THRESHOLD,

@@ -213,6 +213,15 @@ int fr_has_match(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* 
  * the start-offset partition (the OR over shards equals has_match). */
 int fr_has_match_range(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
                        size_t start_hi, fr_ct* out, fr_match_stats* stats);
+/* Same start range, the result as *n_parts <= max_parts booleans out[0..n_parts) whose OR
+ * is fr_has_match_range's result (round 5).  The threshold lowering's OR tree over the
+ * range's start offsets (engine.rs:22-35) stops once <= max_parts literals remain, so a
+ * caller OR-ing the parts of W start shards (W * max_parts <= 16: one threshold OR) spends
+ * the tree's last level once instead of once per shard plus once to combine.  Faithful
+ * lowerings, and roots that are not an OR, give one part.  1 <= max_parts <= 16; out has
+ * room for max_parts handles; each part is a boolean handle of its own. */
+int fr_has_match_parts(fr_ctx* ctx, const fr_ct* content, size_t n_chars, const char* pattern, size_t start_lo,
+                       size_t start_hi, size_t max_parts, fr_ct* out, size_t* n_parts, fr_match_stats* stats);
 /* n_matches independent has_match calls of one pattern over n_matches contents
  * of n_chars each (content[m * n_chars + q], out[m]): the matches' circuits run
  * as one plan, so each dependency level of all matches shares its launches
@@ -315,6 +324,12 @@ typedef struct {
 int fr_schedule_match(size_t n_chars, const char* pattern, size_t start_lo, size_t start_hi, int32_t lowering,
                       int32_t engine, int32_t grammar, int32_t multi_value, fr_job* jobs, size_t jobs_cap,
                       size_t* n_jobs, uint32_t* level_off, size_t level_cap, size_t* n_levels, int32_t* out3);
+/* The schedule of fr_has_match_parts' program: outs3[3j .. 3j+2] = part j's (out_gate,
+ * out_w, out_const), j < *n_parts (outs3 has room for 3 * max_parts). */
+int fr_schedule_match_parts(size_t n_chars, const char* pattern, size_t start_lo, size_t start_hi, int32_t lowering,
+                            int32_t engine, int32_t grammar, int32_t multi_value, size_t max_parts, fr_job* jobs,
+                            size_t jobs_cap, size_t* n_jobs, uint32_t* level_off, size_t level_cap, size_t* n_levels,
+                            int32_t* outs3, size_t* n_parts);
 
 /* ----- host-only introspection (tests; no device needed) ----- */
 /* Canonical AST string of parse(pattern) (parser.rs:146-185). */
@@ -351,6 +366,11 @@ int fr_set_grammar(fr_ctx* ctx, int32_t grammar);
 int fr_parse_ex(const char* pattern, int32_t grammar, char* buf, size_t buflen);
 int fr_plain_match_g(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                      int32_t lowering, int32_t engine, int32_t grammar, fr_plain_result* out);
+/* fr_plain_match_g of fr_has_match_parts' program: out->result_lowered is the OR of the
+ * parts, parts[0..*n_parts) their plaintext values (room for max_parts). */
+int fr_plain_match_parts(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
+                         int32_t lowering, int32_t engine, int32_t grammar, size_t max_parts, fr_plain_result* out,
+                         int32_t* parts, size_t* n_parts);
 int fr_set_engine(fr_ctx* ctx, int32_t engine);
 int fr_plain_match_ex(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                       int32_t lowering, int32_t engine, fr_plain_result* out);

@@ -315,11 +315,21 @@ class Oracle:
                 for f in range(j.n_out):
                     val[j.out_gate[f]] = outs[k]
                     k += 1
+        return self._output(S.out_gate, S.out_w, S.out_const)
+
+    def _output(self, gate, w, cst) -> np.ndarray:
+        """a program output cst + w * gate from the last run's gate values (a linear op)"""
         out = np.zeros(self.big + 1, dtype=np.uint64)
-        if S.out_gate >= 0:
-            out = (np.uint64(S.out_w & 0xFFFFFFFFFFFFFFFF) * val[S.out_gate]).astype(np.uint64)
-        out[-1] += np.uint64((S.out_const << 59) & 0xFFFFFFFFFFFFFFFF)
+        if gate >= 0:
+            out = (np.uint64(w & 0xFFFFFFFFFFFFFFFF) * self.sched_val[gate]).astype(np.uint64)
+        out[-1] += np.uint64((cst << 59) & 0xFFFFFFFFFFFFFFFF)
         return out
+
+    def run_schedule_parts(self, S, content_lwes: np.ndarray) -> list:
+        """run_schedule of a parts schedule (fheregex.schedule_match max_parts > 1): the
+        LWE of every part"""
+        self.run_schedule(S, content_lwes)
+        return [self._output(*p) for p in S.parts]
 
     @staticmethod
     def set_threads(t: int):

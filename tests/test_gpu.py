@@ -912,6 +912,83 @@ def test_match_words_start_shards(gctx, oracle_k1, world):
         gctx.release(h)
 
 
+@pytest.mark.parametrize("world", [2, 4])
+def test_match_parts_words_start_shards(gctx, oracle_k1, world):
+    """fr_has_match_parts word for word: each rank's 16 // world parts (its OR tree stopped
+    one level early) against the oracle's evaluation of the same parts schedule on the same
+    LWEs, then ONE threshold OR over every rank's parts (Context.or_each) against the
+    oracle's gate: the unsharded match's level count, and its result.  /the/i on 192
+    letters, "ThE" across the first shard boundary."""
+    L, pat = 192, "/the/i"
+    P = 16 // world
+    rng = np.random.default_rng(83 + world)
+    alpha = np.frombuffer(b"abcdefghijklmnopqrstuvwxyzABCDEFGHIJKLMNOPQRSTUVWXYZ ", dtype=np.uint8)
+    s = bytearray(rng.choice(alpha, L))
+    for i in range(L - 2):
+        if bytes(s[i:i + 3]).lower() == b"the":
+            s[i + 2] = ord("x")
+    cut = F.shard_starts(L, world, 1)[0]
+    s[cut - 1:cut + 2] = b"ThE"
+    s = bytes(s)
+    O = oracle_k1
+    words, parts, held = [], [], []
+    levels_full = F.schedule_match(L, pat)
+    for r in range(world):
+        lo, hi = F.shard_starts(L, world, r)
+        wlo, whi = F.content_window(L, pat, lo, hi)
+        win = gctx.encrypt_str(s[wlo:whi], seed=90 + r)
+        full = np.zeros((L, 4, gctx.lwe_len), dtype=np.uint64)
+        full[wlo:whi] = win
+        hs = [F.NULL_CT] * L
+        hs[wlo:whi] = gctx.upload_radix(win)
+        outs, st = gctx.has_match_parts(hs, pat, lo, hi, P)
+        S = F.schedule_match(L, pat, lo, hi, max_parts=P)
+        assert 1 <= len(outs) == len(S.parts) <= P
+        assert (len(S.jobs), len(S.level_off) - 1) == (st.blind_rotations, st.levels)
+        exp = O.run_schedule_parts(S, full)
+        for j, o in enumerate(outs):
+            assert np.array_equal(gctx.download_radix(o)[0], exp[j]), (r, j)
+        r_exp = int(any(s[i:i + 3].lower() == b"the" for i in range(lo, hi)))
+        assert int(any(O.decode16(e)[0] for e in exp)) == r_exp, r
+        words += exp
+        parts += outs
+        held += hs[wlo:whi]
+    assert st.levels + 1 == len(levels_full.level_off) - 1  # the last rank's levels + the OR
+    res = gctx.or_each([parts])[0]
+    exp_or = O.gates([([(q, 1) for q in range(len(parts))], -1, [0] * 16, 2)], np.stack(words))[0]
+    assert np.array_equal(gctx.download_radix(res)[0], exp_or)
+    assert O.decode16(exp_or)[0] == 1 == ro.has_match_reach(s.decode(), pat)
+    for h in held + parts + [res]:
+        gctx.release(h)
+
+
+def test_match_parts_cached_and_uncached_bit_identical(gctx):
+    """fr_has_match_parts from a cached plan (its parts are fresh copies of the plan's gate
+    slots) and with the plan cache off (parts copied out before the plan's slots are
+    freed): the same words, <= max_parts parts, OR = fr_has_match_range's result"""
+    rng = np.random.default_rng(87)
+    s = _printable(rng, 96).replace("abc", "abd")
+    s = s[:40] + "abc" + s[43:]
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=88))
+    runs = []
+    for cache in (8, 8, 0):
+        gctx.set_plan_cache(cache)
+        outs, st = gctx.has_match_parts(hs, "/abc/", 16, 80, 16)
+        runs.append(([gctx.download_radix(o) for o in outs], st.plan_cached))
+        for o in outs:
+            gctx.release(o)
+    gctx.set_plan_cache(8)
+    assert [c for _, c in runs] == [0, 1, 0]
+    w0 = runs[0][0]
+    assert 1 < len(w0) <= 16
+    for w, _ in runs[1:]:
+        assert len(w) == len(w0) and all(np.array_equal(a, b) for a, b in zip(w, w0))
+    one, _ = gctx.has_match(hs, "/abc/", 16, 80)
+    assert int(any(gctx.decrypt_radix(w) for w in w0)) == gctx.decrypt_radix(gctx.download_radix(one)) == 1
+    for h in hs + [one]:
+        gctx.release(h)
+
+
 # ------------------------------------- start-offset shards across contexts
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("where", ["boundary", "absent"])

@@ -177,6 +177,66 @@ def test_start_range_partition_is_or():
         assert full == (a | b), (c, p, cut)
 
 
+def test_match_parts_or_to_the_range_result():
+    """fr_has_match_parts' program (host side): <= max_parts parts whose OR is the range's
+    result (engine.rs:22-35 fold), on random patterns, ranges and part counts; faithful
+    lowerings and max_parts = 1 give the one-output program unchanged"""
+    rng = random.Random(31)
+    n = 0
+    while n < 300:
+        p = rf.rand_pattern(rng)
+        c = rf.rand_content(rng, rng.randint(1, 9))
+        lo = rng.randint(0, len(c))
+        hi = rng.randint(lo, len(c))
+        P = rng.choice([1, 2, 3, 4, 8, 16])
+        low = rng.choice([F.LOWER_THRESHOLD, F.LOWER_THRESHOLD, F.LOWER_FAITHFUL, F.LOWER_FAITHFUL_TREE])
+        try:
+            base = F.plain_match(c, p, low, start_lo=lo, start_hi=hi)
+        except (F.ParseError, F.ReferencePanic):
+            continue
+        if base.n_branches > 500:
+            continue
+        r, vals = F.plain_match_parts(c, p, lo, hi, P, lowering=low)
+        assert 1 <= len(vals) <= P and set(vals) <= {0, 1}, (c, p, P, vals)
+        assert r.result_lowered == int(any(vals)) == base.result_lowered == base.result_recorded, (c, p, lo, hi, P)
+        assert r.levels <= base.levels and r.pbs <= base.pbs, (c, p, P)
+        if P == 1 or low != F.LOWER_THRESHOLD:
+            assert len(vals) == 1 and (r.pbs, r.levels) == (base.pbs, base.levels), (c, p, P, low)
+        n += 1
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_match_parts_save_the_combine_level(world):
+    """/abc/ on 256 chars split by start offsets over `world` ranks with 16 // world parts
+    each: every rank's program is one level shorter (the OR tree stops at its parts), so
+    the ranks plus the one threshold OR over world * parts <= 16 booleans take the
+    unsharded match's 4 levels, not 5; the parts' OR is the rank's range result"""
+    import bench
+    c = bench.make_content("printable", 256, seed=0)
+    c = c[:77] + b"abc" + c[80:]
+    P = 16 // world
+    got = []
+    for r in range(world):
+        lo, hi = F.shard_starts(256, world, r)
+        base = F.plain_match(c, "/abc/", start_lo=lo, start_hi=hi)
+        pr, vals = F.plain_match_parts(c, "/abc/", lo, hi, P)
+        assert (base.levels, pr.levels) == (4, 3) and len(vals) <= P, (r, base.levels, pr.levels, vals)
+        assert pr.pbs == base.pbs - 1
+        S = F.schedule_match(256, "/abc/", lo, hi, max_parts=P)
+        assert len(S.parts) == len(vals) and len(S.level_off) - 1 == 3
+        assert int(any(vals)) == base.result_recorded == int(any(c[i:i + 3] == b"abc" for i in range(lo, hi)))
+        got.append(int(any(vals)))
+    assert sum(got) >= 1 and F.plain_match(c, "/abc/").levels == 4
+
+
+def test_match_parts_rejects_bad_counts():
+    for P in (0, 17):
+        with pytest.raises(F.FheRegexError):
+            F.plain_match_parts("abcabc", "/abc/", 0, 6, P)
+        with pytest.raises(F.FheRegexError):
+            F.schedule_match(6, "/abc/", 0, 6, max_parts=P)
+
+
 def test_scalar_maps_match_oracle():
     """Product scalar maps (Montgomery CRT, reciprocal digit, residue -> torus)
     vs the oracle's plain 128-bit definitions."""
