@@ -705,10 +705,10 @@ def main():
                 ctx.release(h)  # stream-ordered: a later user of its slot runs after the export
             t2 = time.perf_counter()
             if rccl:
-                dist.all_gather_into_tensor(recv[i].view(-1), send[i])
+                dist.all_gather_into_tensor(recv[i].view(-1), send[i].view(-1))
             else:
-                for r, b in enumerate(gather(send[i])):
-                    recv[i, r].copy_(b)
+                for r, b in enumerate(gather(send[i].view(-1))):
+                    recv[i, r].copy_(b.view(P, -1))
             if times is not None:
                 times["starts_ms"] = times.get("starts_ms", 0.0) + (t2 - t) * 1e3
                 times["gather_ms"] = times.get("gather_ms", 0.0) + (time.perf_counter() - t2) * 1e3
