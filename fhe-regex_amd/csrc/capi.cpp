@@ -1372,6 +1372,19 @@ int fr_has_match_parts(fr_ctx* ctx, const fr_ct* content, size_t n, const char* 
     })
 }
 
+int fr_debug_enumeration_cost(const char* pattern, int32_t grammar, size_t n_chars, size_t lo, size_t hi,
+                              uint64_t cap, int32_t enumerate, uint64_t* counted, uint64_t* enumerated) {
+    FR_TRY({
+        NEED(pattern && counted && enumerated && lo <= hi && cap < UINT64_MAX);
+        NEED(grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT);
+        GrammarScope scope(grammar);
+        ReP re = parse(pattern);
+        uint64_t c = 0;
+        *counted = enumeration_cost(n_chars, re, lo, hi, cap, &c) ? c : UINT64_MAX;
+        *enumerated = enumerate ? enumeration_spent(n_chars, re, lo, hi, cap) : 0;
+    })
+}
+
 int fr_plain_match_parts(const char* content, size_t len, const char* pattern, size_t lo, size_t hi, int32_t lowering,
                          int32_t engine, int32_t grammar, size_t max_parts, fr_plain_result* out, int32_t* parts,
                          size_t* n_parts) {

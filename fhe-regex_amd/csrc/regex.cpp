@@ -5,6 +5,8 @@
 //   Execution:   src/regex/execution.rs:64-222
 #include "regex.h"
 
+#include <algorithm>
+#include <map>
 #include <sstream>
 
 namespace fr {
@@ -736,14 +738,190 @@ Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, s
     return out;
 }
 
+// ------------------------------------------------------------ enumeration cost
+namespace {
+struct DryPanic {};  // the enumeration would panic here: no count
+struct DryRes {
+    std::vector<std::pair<size_t, uint64_t>> ends;  // (end position, multiplicity), ascending
+    uint64_t spent = 0;                             // spend() total of one call
+    uint64_t size = 0;                              // branches one call returns
+};
+// build_branches without the branches: every case mirrors its line above; sums and
+// products saturate at cap
+struct Dry {
+    size_t L;
+    uint64_t cap;
+    std::map<std::pair<const Re*, size_t>, DryRes> memo;  // node references stay valid
+
+    uint64_t add(uint64_t a, uint64_t b) const { return a >= cap || b >= cap || a + b >= cap ? cap : a + b; }
+    uint64_t mul(uint64_t a, uint64_t b) const {
+        if (!a || !b) return 0;
+        return a >= cap || b >= cap || a > cap / b ? cap : std::min(cap, a * b);
+    }
+    void put(std::map<size_t, uint64_t>& m, size_t e, uint64_t c) const {
+        uint64_t& v = m[e];
+        v = add(v, c);
+    }
+    uint64_t total(const std::map<size_t, uint64_t>& m) const {
+        uint64_t t = 0;
+        for (auto& [e, c] : m) t = add(t, c);
+        return t;
+    }
+    // the branches of bb(x, end) over every (end, multiplicity) of conts; spends into *spent
+    std::map<size_t, uint64_t> extend(const std::map<size_t, uint64_t>& conts, const Re* x, uint64_t* spent) {
+        std::map<size_t, uint64_t> nxt;
+        for (auto& [e, c] : conts) {
+            const DryRes& r = bb(x, e);
+            *spent = add(*spent, mul(c, r.spent));
+            for (auto& [e2, c2] : r.ends) put(nxt, e2, mul(c, c2));
+        }
+        return nxt;
+    }
+    static std::map<size_t, uint64_t> as_map(const DryRes& r) { return {r.ends.begin(), r.ends.end()}; }
+    DryRes done(const std::map<size_t, uint64_t>& m, uint64_t spent) const {
+        DryRes r;
+        r.ends.assign(m.begin(), m.end());
+        r.spent = spent;
+        r.size = total(m);
+        return r;
+    }
+    const DryRes& bb(const Re* re, size_t p) {
+        const auto key = std::make_pair(re, p);
+        auto it = memo.find(key);
+        if (it != memo.end()) return it->second;
+        DryRes r = compute(re, p);
+        return memo.emplace(key, std::move(r)).first->second;
+    }
+    DryRes compute(const Re* re, size_t p) {
+        std::map<size_t, uint64_t> out;
+        switch (re->kind) {
+            case Re::SOF:
+                if (p == 0) put(out, p, 1);
+                return done(out, 0);
+            case Re::EOF_:
+                if (p == L) put(out, p, 1);
+                return done(out, 0);
+            default: break;
+        }
+        if (p >= L) return done(out, 0);
+        switch (re->kind) {
+            case Re::CHAR:
+            case Re::ANY:
+            case Re::BETWEEN:
+            case Re::RANGE:
+            case Re::CLASS: put(out, p + 1, 1); return done(out, 0);
+            case Re::NOT: return bb(re->a.get(), p);
+            case Re::EITHER: {
+                const DryRes& l = bb(re->a.get(), p);
+                uint64_t spent = l.spent;
+                out = as_map(l);
+                const DryRes& r = bb(re->b.get(), p);
+                spent = add(spent, r.spent);
+                for (auto& [e, c] : r.ends) put(out, e, c);
+                return done(out, spent);
+            }
+            case Re::OPTIONAL: {
+                const DryRes& r = bb(re->a.get(), p);
+                out = as_map(r);
+                put(out, p, 1);
+                return done(out, r.spent);
+            }
+            case Re::SEQ: {
+                if (re->xs.empty()) throw DryPanic{};
+                const DryRes& r0 = bb(re->xs[0].get(), p);
+                uint64_t spent = r0.spent;
+                std::map<size_t, uint64_t> conts = as_map(r0);
+                for (size_t i = 1; i < re->xs.size(); ++i) {
+                    conts = extend(conts, re->xs[i].get(), &spent);
+                    spent = add(spent, total(conts));
+                }
+                return done(conts, spent);
+            }
+            case Re::REPEATED: {
+                const uint64_t at_least = re->has_lo ? re->lo : 0;
+                const uint64_t at_most = re->has_hi ? re->hi : (uint64_t)(L - p);
+                if (at_least > at_most) return done(out, 0);
+                if (at_least == 0) put(out, p, 1);
+                const uint64_t reps = at_least > 1 ? at_least : 1;
+                if (reps > (1u << 24)) throw DryPanic{};
+                // the Seq of reps copies
+                const Re* a = re->a.get();
+                const DryRes& r0 = bb(a, p);
+                uint64_t spent = r0.spent;
+                std::map<size_t, uint64_t> conts = as_map(r0);
+                for (uint64_t r = 1; r < reps && !conts.empty() && spent < cap; ++r) {
+                    conts = extend(conts, a, &spent);
+                    spent = add(spent, total(conts));
+                }
+                for (auto& [e, c] : conts) put(out, e, c);
+                // at_least + 1 ..= at_most, stopping after the first empty step (or once
+                // saturated: the count is then past cap whatever follows)
+                for (uint64_t it = at_least + 1; it <= at_most && spent < cap; ++it) {
+                    std::map<size_t, uint64_t> nxt = extend(conts, a, &spent);
+                    spent = add(spent, total(nxt));
+                    if (nxt.empty()) break;
+                    for (auto& [e, c] : nxt) put(out, e, c);
+                    conts = std::move(nxt);
+                }
+                return done(out, spent);
+            }
+            default: break;
+        }
+        throw DryPanic{};  // unmatched variant: the enumeration reports it
+    }
+};
+}  // namespace
+
+uint64_t enumeration_spent(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap) {
+    if (hi > L) hi = L;
+    const size_t saved = g_budget;
+    g_budget = cap;
+    uint64_t spent;
+    try {
+        for (size_t i = lo; i < hi; ++i) spend(build_branches(L, re, i).size());  // record_has_match's loop
+        spent = cap - g_budget;
+    } catch (const Error& e) {
+        g_budget = saved;
+        if (e.code != FR_ERR_OOM) throw;
+        return cap + 1;
+    }
+    g_budget = saved;
+    return spent;
+}
+
+bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost) {
+    if (hi > L) hi = L;
+    Dry d{L, cap == UINT64_MAX ? cap : cap + 1, {}};
+    uint64_t t = 0;
+    try {
+        for (size_t i = lo; i < hi && t < d.cap; ++i) {  // record_has_match: spend(bs.size()) per start
+            const DryRes& r = d.bb(re.get(), i);
+            t = d.add(t, d.add(r.spent, r.size));
+        }
+    } catch (const DryPanic&) {
+        return false;
+    }
+    *cost = t;
+    return true;
+}
+
 Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
                                  int engine) {
     if (engine == FR_ENGINE_MERGED) return record_has_match_merged(dag, L, pattern, lo, hi);
     if (engine == FR_ENGINE_ENUMERATE) return record_has_match(dag, L, pattern, lo, hi);
     // AUTO: the reference's enumeration (exact counters) while it stays within
-    // a few million variants, else the state-merging evaluator
+    // a few million variants, else the state-merging evaluator.  The enumeration's cost
+    // is counted first (enumeration_cost, exact), so a pattern past the budget goes
+    // straight to the merged evaluator instead of building 2^22 branches and dropping
+    // them (config 5 at 512 chars: ~1 s of host time per cold call)
+    constexpr size_t budget = (size_t)1 << 22;
+    {
+        uint64_t cost = 0;
+        if (enumeration_cost(L, parse(pattern), lo, hi, budget, &cost) && cost > budget)
+            return record_has_match_merged(dag, L, pattern, lo, hi);
+    }
     try {
-        return record_has_match(dag, L, pattern, lo, hi, (size_t)1 << 22);
+        return record_has_match(dag, L, pattern, lo, hi, budget);
     } catch (const Error& e) {
         if (e.code != FR_ERR_OOM) throw;
     }

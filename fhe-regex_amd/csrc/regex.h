@@ -163,6 +163,15 @@ struct Recorded {
 // it); the reference itself has no bound and exhausts memory instead.
 Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
                           size_t branch_budget = SIZE_MAX);
+// What record_has_match would spend of its branch budget (the variants it enumerates),
+// counted without building a branch: per (node, position) the multiset of end positions
+// with multiplicities and the spends of one call, memoised, so it is polynomial in L
+// where the enumeration is exponential.  Saturates just past cap.  Returns false (no
+// count) where the enumeration would panic (empty Seq, a repetition count the reference
+// cannot allocate): the caller then enumerates to reproduce the error.
+bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost);
+// The same by enumerating (test hook): the spends, or cap + 1 once past cap.
+uint64_t enumeration_spent(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap);
 // State-merging evaluator (merged.cpp, beyond the reference): the same boolean,
 // polynomial in L.  Error FR_ERR_INVALID for AST shapes it does not cover.
 Recorded record_has_match_merged(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi);

@@ -147,6 +147,8 @@ _SIGS = {
                                           C.c_int32, C.c_int32, C.c_size_t, C.POINTER(FrJob), C.c_size_t,
                                           C.POINTER(C.c_size_t), C.POINTER(C.c_uint32), C.c_size_t,
                                           C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]),
+    "fr_debug_enumeration_cost": (C.c_int, [C.c_char_p, C.c_int32, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
+                                            C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
@@ -272,6 +274,17 @@ def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESH
     _check(lib().fr_plain_match_g(content, len(content), pattern.encode("latin-1"), start_lo, hi, lowering, engine,
                                   grammar, C.byref(r)))
     return r
+
+
+def enumeration_cost(pattern: str, n_chars: int, start_lo: int = 0, start_hi: Optional[int] = None,
+                     cap: int = 1 << 22, enumerate: bool = False, grammar: int = GRAMMAR_REFERENCE):
+    """(counted, enumerated): the reference enumeration's variant count from the AST
+    (None where it would panic) and, if asked, by enumerating; both saturate at cap + 1"""
+    hi = n_chars if start_hi is None else start_hi
+    c, e = C.c_uint64(), C.c_uint64()
+    _check(lib().fr_debug_enumeration_cost(pattern.encode("latin-1"), grammar, n_chars, start_lo, hi, cap,
+                                           int(enumerate), C.byref(c), C.byref(e)))
+    return (None if c.value == 2**64 - 1 else c.value), (e.value if enumerate else None)
 
 
 def plain_match_parts(content: bytes | str, pattern: str, start_lo: int, start_hi: int, max_parts: int,

@@ -229,6 +229,52 @@ def test_match_parts_save_the_combine_level(world):
     assert sum(got) >= 1 and F.plain_match(c, "/abc/").levels == 4
 
 
+def test_enumeration_cost_counts_exactly():
+    """FR_ENGINE_AUTO's decision: the reference enumeration's variant count (engine.rs:45-214,
+    every spend of record_has_match) counted from the AST equals the count of actually
+    enumerating, on random patterns, lengths, start ranges and caps (saturating alike past
+    the cap); patterns whose enumeration panics give no count"""
+    rng = random.Random(41)
+    n = 0
+    while n < 400:
+        p = rf.rand_pattern(rng)
+        L = rng.randint(0, 9)
+        lo = rng.randint(0, L)
+        hi = rng.randint(lo, L)
+        cap = rng.choice([10, 100, 1000, 1 << 22])
+        try:
+            counted, enumerated = F.enumeration_cost(p, L, lo, hi, cap=cap, enumerate=True)
+        except (F.ParseError, F.ReferencePanic):
+            continue
+        if counted is not None:
+            assert counted == enumerated, (p, L, lo, hi, cap, counted, enumerated)
+        n += 1
+    for p, L, exp in [("/abc/", 256, 763), ("/the/i", 1024, 3067), ("/^a{2,8}(bc|de)+[^xyz]$/", 20, 12979)]:
+        assert F.enumeration_cost(p, L, enumerate=True) == (exp, exp), p
+
+
+def test_auto_engine_skips_a_doomed_enumeration():
+    """config 5 at its 512 chars: AUTO counts ~2^252 variants and goes straight to the
+    merged evaluator (round 4 built 2^22 branches first: ~1 s of host time per cold call);
+    the same result and circuit as FR_ENGINE_MERGED"""
+    import time
+    pat = "/^a{2,8}(bc|de)+[^xyz]$/"
+    c = "aaa" + "bc" * 127 + "de" * 127 + "f"
+    c = c[:512]
+    assert F.enumeration_cost(pat, 512) == ((1 << 22) + 1, None)
+    t = time.perf_counter()
+    a = F.plain_match(c, pat, engine=F.ENGINE_AUTO)
+    dt = time.perf_counter() - t
+    m = F.plain_match(c, pat, engine=F.ENGINE_MERGED)
+    assert (a.result_recorded, a.result_lowered, a.ct_ops, a.pbs, a.levels) == \
+        (m.result_recorded, m.result_lowered, m.ct_ops, m.pbs, m.levels)
+    assert dt < 0.5, dt
+    # a pattern within the budget still enumerates (the reference's exact counters)
+    e = F.plain_match("x" * 64 + "abc", "/abc/", engine=F.ENGINE_ENUMERATE)
+    a = F.plain_match("x" * 64 + "abc", "/abc/", engine=F.ENGINE_AUTO)
+    assert (a.ct_ops, a.cache_hits, a.n_branches) == (e.ct_ops, e.cache_hits, e.n_branches)
+
+
 def test_match_parts_rejects_bad_counts():
     for P in (0, 17):
         with pytest.raises(F.FheRegexError):
