@@ -311,7 +311,27 @@ struct Lowerer {
         if (a.k == Form::CONST) return is_and ? (a.c ? std::move(b) : const_form(0)) : (a.c ? const_form(1) : std::move(b));
         if (b.k == Form::CONST) return is_and ? (b.c ? std::move(a) : const_form(0)) : (b.c ? const_form(1) : std::move(a));
         // member lists are sorted (forms keep their literals sorted): merge, O(|a|+|b|)
-        const std::vector<Lit> l0 = members(std::move(a), is_and), r = members(std::move(b), is_and);
+        std::vector<Lit> l0 = members(std::move(a), is_and), r = members(std::move(b), is_and);
+        if (l0.size() < r.size()) std::swap(l0, r);
+        if (r.size() == 1) {
+            // the long folds (has_match's OR over its branches, engine.rs:22-35) add one
+            // literal at a time, usually past the end: insert in place instead of copying
+            // the whole list per operand (quadratic in the branch count)
+            // (a form's own list is sorted, unique and free of x / !x pairs: only x's
+            // neighbours can complement it)
+            const Lit x = r[0];
+            auto it = std::lower_bound(l0.begin(), l0.end(), x);
+            if (it == l0.end() || !(*it == x)) {
+                if ((it != l0.end() && it->gate == x.gate) || (it != l0.begin() && (it - 1)->gate == x.gate))
+                    return const_form(is_and ? 0 : 1);  // x & !x, x | !x
+                l0.insert(it, x);
+            }
+            if (l0.size() == 1) return lit_form(l0[0]);
+            Form f;
+            f.k = is_and ? Form::AND : Form::OR;
+            f.lits = std::move(l0);
+            return f;
+        }
         std::vector<Lit> l;
         l.reserve(l0.size() + r.size());
         std::merge(l0.begin(), l0.end(), r.begin(), r.end(), std::back_inserter(l));

@@ -914,7 +914,14 @@ Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pat
     // is counted first (enumeration_cost, exact), so a pattern past the budget goes
     // straight to the merged evaluator instead of building 2^22 branches and dropping
     // them (config 5 at 512 chars: ~1 s of host time per cold call)
-    constexpr size_t budget = (size_t)1 << 22;
+    // them (config 5 at 512 chars: ~1 s of host time per cold call).  Small enumerations
+    // (/abc/ x 256: 763 variants) are tried directly: counting costs about as much as them.
+    constexpr size_t budget = (size_t)1 << 22, small = (size_t)1 << 12;
+    try {  // (the budget runs out while enumerating, before the dag is touched)
+        return record_has_match(dag, L, pattern, lo, hi, small);
+    } catch (const Error& e) {
+        if (e.code != FR_ERR_OOM) throw;
+    }
     {
         uint64_t cost = 0;
         if (enumeration_cost(L, parse(pattern), lo, hi, budget, &cost) && cost > budget)
