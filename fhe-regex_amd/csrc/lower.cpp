@@ -99,16 +99,36 @@ struct Lowerer {
         return add_gate({1, kind, pos, half, v, tag}, std::move(g));
     }
     // arbitrary 16-entry LUT over the packed nibble (x_{2h} + 4 x_{2h+1}) of char `pos`
+    // (its own index, keyed without a heap-allocated key: the lowering's most frequent lookup)
+    struct NibKey {
+        int32_t pos, half;
+        uint64_t lut_lo, lut_hi;  // the 16 LUT bytes
+        bool operator==(const NibKey& o) const {
+            return pos == o.pos && half == o.half && lut_lo == o.lut_lo && lut_hi == o.lut_hi;
+        }
+    };
+    struct NibKeyHash {
+        size_t operator()(const NibKey& k) const {
+            uint64_t h = (uint64_t)(uint32_t)k.pos * 0x9E3779B97F4A7C15ULL ^ (uint64_t)k.half;
+            h = (h ^ k.lut_lo) * 0xBF58476D1CE4E5B9ULL;
+            h = (h ^ k.lut_hi) * 0x94D049BB133111EBULL;
+            return (size_t)(h ^ (h >> 31));
+        }
+    };
+    std::unordered_map<NibKey, int, NibKeyHash> nib_index;
     int nibble_lut_gate(int pos, int half, const uint8_t* lut) {
-        std::vector<int64_t> key(19);  // (offset 0, LUT kind)
-        key[0] = 6, key[1] = pos, key[2] = half;
-        for (int v = 0; v < 16; ++v) key[3 + v] = lut[v];
-        auto it = gate_index.find(key);
-        if (it != gate_index.end()) return it->second;
+        NibKey key{pos, half, 0, 0};
+        std::memcpy(&key.lut_lo, lut, 8);
+        std::memcpy(&key.lut_hi, lut + 8, 8);
+        auto it = nib_index.find(key);
+        if (it != nib_index.end()) return it->second;
         PGate g;
         g.ins = {{cblock(pos, 2 * half), 1}, {cblock(pos, 2 * half + 1), 4}};
         std::memcpy(g.lut, lut, 16);
-        return add_gate(std::move(key), std::move(g));
+        prog.gates.push_back(std::move(g));
+        const int id = (int)prog.gates.size() - 1;
+        nib_index.emplace(key, id);
+        return id;
     }
     // Lower "char at pos is in S" (S != {} and S != all).  Characters split into
     // nibbles (hi, lo); rows = hi values grouped by their lo-set, columns = lo
