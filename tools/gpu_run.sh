@@ -14,6 +14,7 @@
 #   rehearsal  launcher-free two-rank lines (gloo, both ranks on the box's one GPU): the metric
 #              default (weak start shards + strong_starts), config 4's default (1,024 chars split
 #              by start offsets), config 5's default (closure shards), weak by matches
+#   rehearsal4 the same with four gloo ranks (the metric and config 4; 16 // 4 = 4 parts per rank)
 #   rccl1      the N > 1 start-shard pipeline over a one-rank RCCL group
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -63,6 +64,12 @@ for part in "${P[@]}"; do
       step 500 "$out/rehearsal_2rank_$tag.err" python3 bench.py --gpus 2 --dist-backend gloo --workload $mode \
         --steps 5 --warmup 1 --out "$out/rehearsal_2rank_$tag.json"
       summ "$out/rehearsal_2rank_$tag.json"
+    done ;;
+  rehearsal4)
+    for mode in metric config4; do
+      step 600 "$out/rehearsal_4rank_$mode.err" python3 bench.py --gpus 4 --dist-backend gloo --workload $mode \
+        --steps 3 --warmup 1 --saturate 0 --probe= --out "$out/rehearsal_4rank_$mode.json"
+      summ "$out/rehearsal_4rank_$mode.json"
     done ;;
   rccl1)
     step 300 "$out/rccl1.err" python3 bench.py --one-rank-group --steps 10 --warmup 2 --cpu-sample 0 --inflight 0 \
