@@ -962,6 +962,32 @@ def test_match_parts_words_start_shards(gctx, oracle_k1, world):
         gctx.release(h)
 
 
+@pytest.mark.parametrize("case", [3, 11, 17])
+def test_match_parts_fuzz_scale(gctx, case):
+    """fr_has_match_parts on fuzz_scale.json patterns (500-950 rotations each), the content
+    split into three start ranges with 5 parts each: every part decrypts to its plaintext
+    value in the host's parts program (fr_plain_match_parts), and each range's OR to the
+    range's result"""
+    cse = load("fuzz_scale.json")["cases"][case]
+    s, pat = cse["content"], cse["pattern"]
+    L = len(s)
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=4000 + case))
+    got_any = 0
+    for r in range(3):
+        lo, hi = F.shard_starts(L, 3, r)
+        outs, st = gctx.has_match_parts(hs, pat, lo, hi, 5)
+        pr, vals = F.plain_match_parts(s, pat, lo, hi, 5, engine=F.ENGINE_AUTO)
+        dec = [gctx.decrypt_radix(gctx.download_radix(o)) for o in outs]
+        assert dec == vals, (r, dec, vals)
+        assert int(any(dec)) == pr.result_recorded
+        got_any |= int(any(dec))
+        for o in outs:
+            gctx.release(o)
+    assert got_any == cse["expected"]
+    for h in hs:
+        gctx.release(h)
+
+
 def test_match_parts_cached_and_uncached_bit_identical(gctx):
     """fr_has_match_parts from a cached plan (its parts are fresh copies of the plan's gate
     slots) and with the plan cache off (parts copied out before the plan's slots are
