@@ -692,6 +692,7 @@ Program lower(const ValueDag& dag, int root, int mode, int max_parts) {
     Form f = mode == FR_LOWER_FAITHFUL ? lw.lower_f(root)
              : mode == FR_LOWER_FAITHFUL_TREE ? lw.lower_ft(root) : lw.lower_t(root);
     Program& p = lw.prog;
+    if (f.k == Form::SET) f = lw.expand_set(f);  // (an empty or full set is a constant)
     if (f.k == Form::CONST) {
         p.outs.push_back(ProgOut{-1, 0, f.c});
     } else {
