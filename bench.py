@@ -23,9 +23,11 @@ their status; under an external launcher WORLD_SIZE must equal --gpus.
     north_star's per-start-offset variants with a final bitor over RCCL): the content
     is --chars per GPU (the workload's length by default, so N x 256 chars for the
     metric), rank r owns start offsets [r chars, (r+1) chars) and holds only the
-    content window those starts read; each rank matches its start range
-    (fr_has_match_range), the per-rank booleans are all-gathered device to device and
-    OR-ed on rank 0 (fr_or_many: the reference's ct_or fold, engine.rs:22-35).  The
+    content window those starts read; each rank matches its start range as up to
+    16 // N booleans (fr_has_match_parts: its OR tree stops where the ranks' one threshold
+    OR takes over; --start-parts 1: fr_has_match_range's single boolean), the booleans are
+    all-gathered device to device and OR-ed on rank 0 (the reference's ct_or fold,
+    engine.rs:22-35).  The
     same run also times weak scaling by matches (every rank its own full-length
     match, no data-path collective) into `weak_matches`, never `value`.
     --shard matches makes that the timed mode.
