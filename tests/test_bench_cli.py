@@ -133,13 +133,16 @@ def test_one_rank_rccl_group_pipeline():
 
 
 @pytest.mark.gpu
-def test_two_gloo_ranks_config4_named_length():
+@pytest.mark.parametrize("parts", [0, 1])
+def test_two_gloo_ranks_config4_named_length(parts):
     """BASELINE config 4 at N = 2 (two gloo ranks sharing the box's GPU): `value` is measured on
     the named 1,024 characters split by start offsets (strong scaling), one JSON line, every
-    step's OR decrypting to the expected bit, both ranks reporting"""
+    step's OR decrypting to the expected bit, both ranks reporting; with each rank's parts
+    (--start-parts 0: 16 // 2 = 8, fr_has_match_parts) and with one boolean per rank (1)"""
     res = subprocess.run([sys.executable, BENCH, "--gpus", "2", "--dist-backend", "gloo", "--workload", "config4",
                           "--steps", "2", "--warmup", "1", "--weak-matches-steps", "0", "--probe=", "--saturate", "0",
-                          "--job-timeout", "280"], capture_output=True, text=True, timeout=300, env=_env())
+                          "--start-parts", str(parts), "--job-timeout", "280"], capture_output=True, text=True,
+                         timeout=300, env=_env())
     assert res.returncode == 0, res.stderr[-3000:]
     lines = [ln for ln in res.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, res.stdout
@@ -147,5 +150,6 @@ def test_two_gloo_ranks_config4_named_length():
     assert d["n_gpus"] == 2 and d["config"]["content_chars"] == 1024 and d["scaling"] == "strong"
     assert d["config"]["shard"] == "starts" and d["results_ok_steps"] is True
     assert d["result_decrypted"] == d["result_expected"] == [1]
+    assert d["config"]["start_parts"] == (parts or 8)
     assert len(d["per_rank"]) == 2 and d["strong_starts"] == {"same_as_value": True,
                                                               "note": d["strong_starts"]["note"]}
