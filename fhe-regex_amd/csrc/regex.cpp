@@ -789,6 +789,9 @@ struct Dry {
         const auto key = std::make_pair(re, p);
         auto it = memo.find(key);
         if (it != memo.end()) return it->second;
+        // a huge AST x content: no count (the caller enumerates, as before) rather than a
+        // memo of unbounded size
+        if (memo.size() >= ((size_t)1 << 20)) throw DryPanic{};
         DryRes r = compute(re, p);
         return memo.emplace(key, std::move(r)).first->second;
     }
