@@ -168,7 +168,8 @@ Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, s
 // with multiplicities and the spends of one call, memoised, so it is polynomial in L
 // where the enumeration is exponential.  Saturates just past cap.  Returns false (no
 // count) where the enumeration would panic (empty Seq, a repetition count the reference
-// cannot allocate): the caller then enumerates to reproduce the error.
+// cannot allocate) or past 2^20 memoised (node, position) pairs: the caller then enumerates,
+// which reproduces the error or the exact decision.
 bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost);
 // The same by enumerating (test hook): the spends, or cap + 1 once past cap.
 uint64_t enumeration_spent(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap);
