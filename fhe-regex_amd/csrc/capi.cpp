@@ -840,6 +840,27 @@ int fr_load_client_key(fr_ctx* ctx, const uint8_t* data, size_t len) {
     })
 }
 
+int fr_gen_client_key(fr_ctx* ctx, uint64_t seed) {
+    FR_TRY({
+        NEED(ctx);
+        ctx->ck = gen_client_key(ctx->p, seed);
+        ctx->has_ck = true;
+        ctx->has_sk = false;
+    })
+}
+
+int fr_serialize_client_key(fr_ctx* ctx, uint8_t* buf, size_t cap, size_t* written) {
+    FR_TRY({
+        NEED(ctx && written);
+        if (!ctx->has_ck) throw Error(FR_ERR_NO_KEY, "client key not loaded");
+        const std::vector<uint8_t> b = serialize_client_key(ctx->ck);
+        *written = b.size();
+        if (!buf) return FR_OK;  // size query
+        NEED(cap >= b.size());
+        std::memcpy(buf, b.data(), b.size());
+    })
+}
+
 int fr_gen_server_key(fr_ctx* ctx, uint64_t seed) {
     FR_TRY({
         NEED(ctx);

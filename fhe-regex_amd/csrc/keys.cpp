@@ -83,8 +83,11 @@ ClientKey parse_client_key(const uint8_t* d, size_t len) {
     off += 8 + 8 * nb;
     uint64_t ng = u(off);
     if (ng > (len - off - 8) / 8) throw Error(FR_ERR_INVALID, "client key: truncated");
-    off += 8 + 8 * ng;                 // GLWE key data (identical to the big key)
-    off += 8;                          // polynomial_size
+    ck.s_glwe.resize(ng);              // GLWE key data (identical to the big key)
+    for (uint64_t i = 0; i < ng; ++i) ck.s_glwe[i] = u(off + 8 + 8 * i);
+    off += 8 + 8 * ng;
+    ck.glwe_poly_size = u(off);        // polynomial_size
+    off += 8;
     uint64_t ns = u(off);
     if (ns == 0 || ns > (1u << 16)) throw Error(FR_ERR_INVALID, "client key: bad small key length");
     if (ns > (len - off - 8) / 8) throw Error(FR_ERR_INVALID, "client key: truncated");
@@ -104,6 +107,7 @@ ClientKey parse_client_key(const uint8_t* d, size_t len) {
     ck.message_modulus = u(off + 112);
     ck.carry_modulus = u(off + 120);
     ck.num_blocks = u(off + 128);
+    for (int i = 0; i < 17; ++i) ck.raw_params[i] = u(off + 8 * (size_t)i);
     if (off + 136 != len) throw Error(FR_ERR_INVALID, "client key: unexpected length");
     for (auto b : ck.s_big)
         if (b > 1) throw Error(FR_ERR_INVALID, "client key: non-binary big key");
@@ -111,6 +115,64 @@ ClientKey parse_client_key(const uint8_t* d, size_t len) {
         if (b > 1) throw Error(FR_ERR_INVALID, "client key: non-binary small key");
     if ((uint64_t)ck.n != ns || (uint64_t)ck.k * ck.N != nb)
         throw Error(FR_ERR_INVALID, "client key: inconsistent dimensions");
+    return ck;
+}
+
+std::vector<uint8_t> serialize_client_key(const ClientKey& ck) {
+    std::vector<uint8_t> out;
+    out.reserve(8 * (ck.s_big.size() + ck.s_glwe.size() + ck.s_small.size() + 21));
+    auto put = [&](uint64_t v) {
+        uint8_t b[8];
+        std::memcpy(b, &v, 8);
+        out.insert(out.end(), b, b + 8);
+    };
+    auto put_vec = [&](const std::vector<uint64_t>& v) {  // bincode Vec<u64>: u64 length, then the words
+        put(v.size());
+        for (uint64_t x : v) put(x);
+    };
+    put_vec(ck.s_big);        // lwe_secret_key (the flattened GLWE key)
+    put_vec(ck.s_glwe);       // glwe_secret_key: data ...
+    put(ck.glwe_poly_size);   // ... and polynomial_size
+    put_vec(ck.s_small);      // lwe_secret_key_after_ks
+    for (uint64_t w : ck.raw_params) put(w);  // Parameters (16 words) + num_blocks
+    return out;
+}
+
+ClientKey gen_client_key(const Params& p, uint64_t seed) {
+    auto bits = [](double x) {
+        uint64_t v;
+        std::memcpy(&v, &x, 8);
+        return v;
+    };
+    ClientKey ck;
+    const size_t big = (size_t)p.big();
+    Rng r(seed, STREAM_CLIENT_KEY);
+    // tfhe-rs draws both secret keys as uniform binary vectors; bit 63 of ChaCha word i
+    ck.s_big.resize(big);
+    for (size_t i = 0; i < big; ++i) ck.s_big[i] = r.u64(i) >> 63;
+    ck.s_small.resize((size_t)p.n);
+    for (size_t t = 0; t < (size_t)p.n; ++t) ck.s_small[t] = r.u64(big + t) >> 63;
+    ck.s_glwe = ck.s_big;
+    ck.glwe_poly_size = (uint64_t)p.N;
+    ck.n = p.n;
+    ck.k = p.k;
+    ck.N = p.N;
+    ck.pbs_base_log = p.pbs_base_log;
+    ck.pbs_level = p.pbs_level;
+    ck.ks_base_log = p.ks_base_log;
+    ck.ks_level = p.ks_level;
+    ck.lwe_sigma = p.lwe_sigma;
+    ck.glwe_sigma = p.glwe_sigma;
+    ck.message_modulus = 4;
+    ck.carry_modulus = 4;
+    ck.num_blocks = 4;
+    const uint64_t raw[17] = {(uint64_t)p.n, (uint64_t)p.k, (uint64_t)p.N, bits(p.lwe_sigma), bits(p.glwe_sigma),
+                              (uint64_t)p.pbs_base_log, (uint64_t)p.pbs_level, (uint64_t)p.ks_base_log,
+                              (uint64_t)p.ks_level,
+                              1, 23, bits(p.glwe_sigma),  // pfks_level, pfks_base_log, pfks sigma
+                              0, 0,                       // cbs_level, cbs_base_log
+                              ck.message_modulus, ck.carry_modulus, ck.num_blocks};
+    std::memcpy(ck.raw_params, raw, sizeof raw);
     return ck;
 }
 

@@ -19,6 +19,7 @@ enum Stream : uint64_t {
     STREAM_BSK_NOISE = 4,
     STREAM_ENC_MASK = 5,
     STREAM_ENC_NOISE = 6,
+    STREAM_CLIENT_KEY = 7,
 };
 
 class Rng {
@@ -42,10 +43,26 @@ struct ClientKey {
     int pbs_base_log = 0, pbs_level = 0, ks_base_log = 0, ks_level = 0;
     double lwe_sigma = 0, glwe_sigma = 0;
     uint64_t message_modulus = 0, carry_modulus = 0, num_blocks = 0;
+    // the remaining words of the bincode layout, kept as read so that
+    // serialize_client_key(parse_client_key(b)) == b: the GLWE key's own data
+    // (equal to s_big in every tfhe-rs key) and polynomial_size, and the 17 words
+    // of the parameter block + num_blocks (offsets 38736..38871)
+    std::vector<uint64_t> s_glwe;
+    uint64_t glwe_poly_size = 0;
+    uint64_t raw_params[17] = {};
 };
 
 // Parse the bincode RadixClientKey of the reference fixture.
 ClientKey parse_client_key(const uint8_t* data, size_t len);
+// The same layout written back (engine.rs:238-246 generate_test_keys: bincode::serialize
+// of the RadixClientKey); byte-identical to the blob a key was parsed from.
+std::vector<uint8_t> serialize_client_key(const ClientKey& ck);
+// A fresh RadixClientKey (gen_keys_radix(&PARAM_MESSAGE_2_CARRY_2, 4), ciphertext.rs:42-45):
+// uniform binary GLWE key of k*N bits (its flattening is the big LWE key) and uniform binary
+// LWE key of n bits, from a ChaCha20 stream of `seed` (STREAM_CLIENT_KEY); parameter block
+// from p (PARAM_MESSAGE_2_CARRY_2's words at the default params: pfks = (1, 2^23, glwe
+// sigma), cbs = (0, 0), message and carry modulus 4, 4 blocks).
+ClientKey gen_client_key(const Params& p, uint64_t seed);
 
 // KSK: [i in kN][level j][t in n+1], torus 2^64.
 void gen_ksk(const Params& p, const ClientKey& ck, uint64_t seed, std::vector<uint64_t>& ksk);

@@ -107,6 +107,8 @@ _SIGS = {
     "fr_last_error": (C.c_char_p, []),
     "fr_default_params": (C.c_int, [C.POINTER(Params)]),
     "fr_load_client_key": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t]),
+    "fr_gen_client_key": (C.c_int, [C.c_void_p, C.c_uint64]),
+    "fr_serialize_client_key": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]),
     "fr_gen_server_key": (C.c_int, [C.c_void_p, C.c_uint64]),
     "fr_set_keygen": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_export_server_key": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
@@ -333,6 +335,20 @@ class Context:
     # keys
     def load_client_key(self, blob: bytes):
         _check(lib().fr_load_client_key(self.h, blob, len(blob)))
+
+    def gen_client_key(self, seed: int):
+        """gen_keys_radix(&PARAM_MESSAGE_2_CARRY_2, 4) (ciphertext.rs:44): a fresh
+        uniform binary client key, reproducible from `seed`."""
+        _check(lib().fr_gen_client_key(self.h, seed & 0xFFFFFFFFFFFFFFFF))
+
+    def serialize_client_key(self) -> bytes:
+        """bincode RadixClientKey (engine.rs:238-246 generate_test_keys): the layout
+        load_client_key reads; a loaded key comes back byte for byte."""
+        n = C.c_size_t()
+        _check(lib().fr_serialize_client_key(self.h, None, 0, C.byref(n)))
+        buf = C.create_string_buffer(n.value)
+        _check(lib().fr_serialize_client_key(self.h, buf, n.value, C.byref(n)))
+        return buf.raw
 
     def gen_server_key(self, seed: int):
         """ServerKey::new (engine.rs:252): on the GPU for the FFT ring (KEYGEN_AUTO),
@@ -640,6 +656,10 @@ class ClientKey:
     def decrypt(self, ct: int) -> int:
         return self.ctx.decrypt_radix(self.ctx.download_radix(ct))
 
+    def serialize(self) -> bytes:
+        """bincode::serialize of the RadixClientKey (engine.rs:238-246)."""
+        return self.ctx.serialize_client_key()
+
 
 @dataclass
 class ServerKey:
@@ -649,11 +669,22 @@ class ServerKey:
         return self.ctx.trivial(msg)
 
 
-def gen_keys(client_key_blob: bytes, seed: int = 0, device: int = 0, params: Optional[Params] = None):
-    """gen_keys (ciphertext.rs:42-45) for a given client key: the server key is
-    derived deterministically from `seed` (ServerKey::new, engine.rs:252)."""
+def gen_keys(client_key_blob: Optional[bytes] = None, seed: int = 0, device: int = 0,
+             params: Optional[Params] = None, client_seed: Optional[int] = None):
+    """gen_keys (ciphertext.rs:42-45): (client key, server key).
+
+    Without a blob the client key is fresh (gen_keys_radix(&PARAM_MESSAGE_2_CARRY_2, 4),
+    ciphertext.rs:44), drawn from `client_seed` (default: 64 bits of os.urandom, as the
+    reference draws from the OS); with a blob it is that bincode key (read_test_keys,
+    engine.rs:248-254).  The server key is derived deterministically from `seed`
+    (ServerKey::new, engine.rs:252)."""
     ctx = Context(device, params)
-    ctx.load_client_key(client_key_blob)
+    if client_key_blob is None:
+        if client_seed is None:
+            client_seed = int.from_bytes(os.urandom(8), "little")
+        ctx.gen_client_key(client_seed)
+    else:
+        ctx.load_client_key(client_key_blob)
     ctx.gen_server_key(seed)
     return ClientKey(ctx), ServerKey(ctx)
 

@@ -15,8 +15,11 @@
  *   execution.rs:190  sk.smart_bitxor(a, trivial 1)   fr_not
  *   ciphertext.rs:8-30 create_trivial_radix(sk, m)    fr_trivial
  *   ciphertext.rs:42-45 gen_keys_radix(PARAM_MESSAGE_2_CARRY_2, 4)
- *                     / engine.rs:250-252 bincode client key + ServerKey::new
+ *                                                     fr_gen_client_key + fr_gen_server_key
+ *   engine.rs:248-254 read_test_keys: bincode::deserialize + ServerKey::new
  *                                                     fr_load_client_key + fr_gen_server_key
+ *   engine.rs:238-246 generate_test_keys: bincode::serialize(client key)
+ *                                                     fr_serialize_client_key
  *   ciphertext.rs:32-40 encrypt_str / RadixClientKey::encrypt
  *                                                     fr_encrypt_str (client side, test/bench)
  *   mod.rs:17 / engine.rs:289 RadixClientKey::decrypt fr_decrypt_radix (client side)
@@ -110,6 +113,16 @@ int fr_default_params(fr_params* out); /* PARAM_MESSAGE_2_CARRY_2, k=1, N=2048 *
 /* ----- keys ----- */
 /* bincode RadixClientKey (tfhe-rs 0.2 layout, reference test_data/client_key). */
 int fr_load_client_key(fr_ctx* ctx, const uint8_t* bincode, size_t len);
+/* A fresh client key (gen_keys_radix(&PARAM_MESSAGE_2_CARRY_2, 4), ciphertext.rs:44):
+ * uniform binary GLWE key (k*N bits, flattened: the big LWE key) and LWE key (n bits)
+ * drawn from a ChaCha20 stream of `seed` (the reference draws from the OS CSPRNG; a seed
+ * makes the key reproducible), the parameter block of the context's params.  Replaces
+ * any loaded client key and drops the server key. */
+int fr_gen_client_key(fr_ctx* ctx, uint64_t seed);
+/* bincode of the context's client key in the layout fr_load_client_key reads
+ * (engine.rs:238-246 generate_test_keys): for a loaded key, the loaded bytes exactly.
+ * buf == NULL: size query (*written = bytes needed). */
+int fr_serialize_client_key(fr_ctx* ctx, uint8_t* buf, size_t cap, size_t* written);
 /* Deterministic server key (KSK mod 2^64; BSK on the 2^64 torus for the FFT
  * ring, mod Q for the RNS ring) from the client key and a seed
  * (ServerKey::new, engine.rs:252; gen_keys_radix, ciphertext.rs:44).  With a

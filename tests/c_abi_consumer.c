@@ -75,6 +75,23 @@ int main(int argc, char** argv) {
         unsigned char* blob = (unsigned char*)malloc((size_t)len);
         CHECK(blob && fread(blob, 1, (size_t)len, f) == (size_t)len, "read client key");
         CHECK(fr_load_client_key(ctx, blob, (size_t)len) == FR_OK, "load client key: %s", fr_last_error());
+        /* the writer gives the fixture back byte for byte (engine.rs:238-246) */
+        size_t need = 0;
+        CHECK(fr_serialize_client_key(ctx, NULL, 0, &need) == FR_OK && need == (size_t)len, "client key size %zu",
+              need);
+        unsigned char* back = (unsigned char*)malloc(need ? need : 1);
+        CHECK(back && fr_serialize_client_key(ctx, back, need, &need) == FR_OK && memcmp(back, blob, need) == 0,
+              "serialize(load(fixture)) == fixture");
+        /* a fresh key (gen_keys_radix, ciphertext.rs:44) round-trips through the loader */
+        fr_ctx* gen = NULL;
+        CHECK(fr_ctx_create(&p, -1, &gen) == FR_OK && gen, "second host context");
+        if (gen && back) {
+            CHECK(fr_gen_client_key(gen, 7) == FR_OK, "gen client key: %s", fr_last_error());
+            CHECK(fr_serialize_client_key(gen, back, need, &need) == FR_OK && need == (size_t)len, "generated size");
+            CHECK(fr_load_client_key(gen, back, need) == FR_OK, "load generated key: %s", fr_last_error());
+            fr_ctx_destroy(gen);
+        }
+        free(back);
         free(blob);
         fr_ct content[1] = {0};
         fr_ct out = 0;
