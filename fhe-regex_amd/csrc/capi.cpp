@@ -398,7 +398,9 @@ static int cblk(int pos, int blk) { return -(1 + pos * 4 + blk); }
 // 2^18 = 4.3 GB at k = 1, FR_PLAN_CACHE_SLOTS); eviction runs before the new plan
 // allocates, and a plan larger than the slot budget runs uncached.
 struct CachedMatch {
-    std::string key;
+    std::string key;           // match_key: every numeric field first, the pattern last
+    size_t parts = 1;          // fr_has_match_parts' max_parts (also in the key)
+    int lane = 0;              // lane whose plan copy this is (0: lane 0; also in the key)
     std::vector<int32_t> sig;  // canonical content shape (content_signature)
     Plan plan;
     size_t n_gates = 0;        // program gates of one match (copy m's gates start at m * n_gates)
@@ -421,11 +423,14 @@ namespace fr {
 
 static void drop_cached(fr_ctx* ctx, CachedMatch& e);
 
-static std::string match_key(fr_ctx* ctx, const char* pattern, size_t n, size_t M, size_t lo, size_t hi) {
-    std::string k = std::to_string(ctx->grammar) + "|" + std::to_string(ctx->engine) + "|" +
-                    std::to_string(ctx->lowering) + "|" + std::to_string((int)ctx->multi_value) + "|" +
-                    std::to_string(n) + "|" + std::to_string(M) + "|" + std::to_string(lo) + "|" + std::to_string(hi) +
-                    "|";
+// The key is a fixed number of '|'-terminated numeric fields followed by the pattern, so a
+// pattern's own text (which may contain '|' and digits) cannot make two keys collide.
+static std::string match_key(fr_ctx* ctx, const char* pattern, size_t n, size_t M, size_t lo, size_t hi,
+                             size_t parts, int lane) {
+    std::string k;
+    for (size_t v : {(size_t)ctx->grammar, (size_t)ctx->engine, (size_t)ctx->lowering, (size_t)ctx->multi_value, n, M,
+                     lo, hi, parts, (size_t)lane})
+        k += std::to_string(v) + "|";
     k += pattern;
     return k;
 }
@@ -548,12 +553,10 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
         }
     } lane_scope{dev};
     if (pc.capacity) {
-        key = match_key(ctx, pattern, n, M, lo, hi);
-        if (parts > 1) key += "|parts" + std::to_string(parts);
-        if (lane) key += "|lane" + std::to_string(lane);
+        key = match_key(ctx, pattern, n, M, lo, hi, parts, lane);
         sig = content_signature(ctx, content, n * M, &cmap);
         for (auto& e : pc.entries)
-            if (e->key == key && e->sig == sig) hit = e.get();
+            if (e->parts == parts && e->lane == lane && e->key == key && e->sig == sig) hit = e.get();
     }
     fr_match_stats local{};
     Recorded rec;
@@ -572,6 +575,8 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
         rec.cache_hits = hit->cache_hits;
         rec.n_branches = hit->n_branches;
         const size_t nO = hit->outs.size();
+        if (nO < 1 || nO > parts)  // the caller's out buffer holds M * parts handles
+            throw Error(FR_ERR_INVALID, "cached plan has more outputs than the caller's parts");
         for (size_t m = 0; m < M; ++m)
             for (size_t j = 0; j < nO; ++j) {
                 const ProgOut& o = hit->outs[j];
@@ -621,6 +626,8 @@ static void match_impl(fr_ctx* ctx, const fr_ct* content, size_t n, size_t M, co
             // keep the plan: its slots stay allocated, its batches go to the device once
             auto e = std::make_unique<CachedMatch>();
             e->key = std::move(key);
+            e->parts = parts;
+            e->lane = lane;
             e->sig = std::move(sig);
             e->n_gates = G;
             e->outs = prog.outs;
@@ -1333,7 +1340,7 @@ int fr_set_lanes(fr_ctx* ctx, int32_t n) {
         // the lanes' plan copies go with the lanes (their slots are held by the cache)
         fr_plan_cache& pc = *ctx->plans;
         for (size_t i = pc.entries.size(); i-- > 0;)
-            if (pc.entries[i]->key.find("|lane") != std::string::npos) {
+            if (pc.entries[i]->lane != 0) {
                 drop_cached(ctx, *pc.entries[i]);
                 pc.entries.erase(pc.entries.begin() + (long)i);
             }
@@ -1394,14 +1401,17 @@ int fr_has_match_parts(fr_ctx* ctx, const fr_ct* content, size_t n, const char* 
 }
 
 int fr_debug_enumeration_cost(const char* pattern, int32_t grammar, size_t n_chars, size_t lo, size_t hi,
-                              uint64_t cap, int32_t enumerate, uint64_t* counted, uint64_t* enumerated) {
+                              uint64_t cap, uint64_t mem_bytes, int32_t enumerate, int32_t* outcome,
+                              uint64_t* counted, uint64_t* enumerated) {
     FR_TRY({
-        NEED(pattern && counted && enumerated && lo <= hi && cap < UINT64_MAX);
+        NEED(pattern && outcome && counted && enumerated && lo <= hi && cap < UINT64_MAX);
         NEED(grammar == FR_GRAMMAR_REFERENCE || grammar == FR_GRAMMAR_EXT);
         GrammarScope scope(grammar);
         ReP re = parse(pattern);
         uint64_t c = 0;
-        *counted = enumeration_cost(n_chars, re, lo, hi, cap, &c) ? c : UINT64_MAX;
+        const CostOutcome o = enumeration_cost(n_chars, re, lo, hi, cap, &c, mem_bytes);
+        *outcome = o == COST_COUNTED ? FR_COST_COUNTED : o == COST_PANIC ? FR_COST_PANIC : FR_COST_MEMORY;
+        *counted = o == COST_COUNTED ? c : 0;
         *enumerated = enumerate ? enumeration_spent(n_chars, re, lo, hi, cap) : 0;
     })
 }

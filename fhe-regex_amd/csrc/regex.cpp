@@ -6,47 +6,72 @@
 #include "regex.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <map>
 #include <sstream>
+#include <vector>
 
 namespace fr {
 
 // =================================================================== AST
-std::string to_string(const Re& r) {
-    std::ostringstream o;
+// appends into one string (a small frame per level: the syntax tree may be
+// MAX_AST_DEPTH deep, e.g. a long alternation's right-nested Either chain)
+static void to_string_into(const Re& r, std::string& o) {
+    auto num = [&](uint64_t v) { o += std::to_string(v); };
     switch (r.kind) {
-        case Re::SOF: o << "SOF"; break;
-        case Re::EOF_: o << "EOF"; break;
-        case Re::ANY: o << "Any"; break;
-        case Re::CHAR: o << "Char(" << (int)r.c << ")"; break;
-        case Re::BETWEEN: o << "Between(" << (int)r.from << "," << (int)r.to << ")"; break;
+        case Re::SOF: o += "SOF"; break;
+        case Re::EOF_: o += "EOF"; break;
+        case Re::ANY: o += "Any"; break;
+        case Re::CHAR: o += "Char("; num(r.c); o += ")"; break;
+        case Re::BETWEEN: o += "Between("; num(r.from); o += ","; num(r.to); o += ")"; break;
         case Re::RANGE:
-            o << "Range(";
-            for (size_t i = 0; i < r.cs.size(); ++i) o << (i ? "," : "") << (int)r.cs[i];
-            o << ")";
+            o += "Range(";
+            for (size_t i = 0; i < r.cs.size(); ++i) { if (i) o += ","; num(r.cs[i]); }
+            o += ")";
             break;
-        case Re::NOT: o << "Not(" << to_string(*r.a) << ")"; break;
-        case Re::EITHER: o << "Either(" << to_string(*r.a) << "," << to_string(*r.b) << ")"; break;
-        case Re::OPTIONAL: o << "Optional(" << to_string(*r.a) << ")"; break;
+        case Re::NOT: o += "Not("; to_string_into(*r.a, o); o += ")"; break;
+        case Re::EITHER: o += "Either("; to_string_into(*r.a, o); o += ","; to_string_into(*r.b, o); o += ")"; break;
+        case Re::OPTIONAL: o += "Optional("; to_string_into(*r.a, o); o += ")"; break;
         case Re::REPEATED:
-            o << "Repeated(" << to_string(*r.a) << ",";
-            if (r.has_lo) o << r.lo; else o << "_";
-            o << ",";
-            if (r.has_hi) o << r.hi; else o << "_";
-            o << ")";
+            o += "Repeated(";
+            to_string_into(*r.a, o);
+            o += ",";
+            if (r.has_lo) num(r.lo); else o += "_";
+            o += ",";
+            if (r.has_hi) num(r.hi); else o += "_";
+            o += ")";
             break;
         case Re::SEQ:
-            o << "Seq(";
-            for (size_t i = 0; i < r.xs.size(); ++i) o << (i ? "," : "") << to_string(*r.xs[i]);
-            o << ")";
+            o += "Seq(";
+            for (size_t i = 0; i < r.xs.size(); ++i) { if (i) o += ","; to_string_into(*r.xs[i], o); }
+            o += ")";
             break;
         case Re::CLASS:
-            o << "Class(";
-            for (size_t i = 0; i + 1 < r.cs.size(); i += 2) o << (i ? "," : "") << (int)r.cs[i] << "-" << (int)r.cs[i + 1];
-            o << ")";
+            o += "Class(";
+            for (size_t i = 0; i + 1 < r.cs.size(); i += 2) { if (i) o += ","; num(r.cs[i]); o += "-"; num(r.cs[i + 1]); }
+            o += ")";
             break;
     }
-    return o.str();
+}
+std::string to_string(const Re& r) {
+    std::string o;
+    to_string_into(r, o);
+    return o;
+}
+
+// Depth of a syntax tree, without recursion (explicit stack).
+static size_t ast_depth(const Re& root) {
+    size_t best = 0;
+    std::vector<std::pair<const Re*, size_t>> st{{&root, 1}};
+    while (!st.empty()) {
+        auto [r, d] = st.back();
+        st.pop_back();
+        best = std::max(best, d);
+        if (r->a) st.push_back({r->a.get(), d + 1});
+        if (r->b) st.push_back({r->b.get(), d + 1});
+        for (auto& x : r->xs) st.push_back({x.get(), d + 1});
+    }
+    return best;
 }
 
 static ReP mk(Re::Kind k) {
@@ -98,11 +123,17 @@ struct PR {
 inline PR ok(ReP n, size_t p) { PR r; r.ok = true; r.pos = p; r.node = std::move(n); return r; }
 inline PR fail(bool committed) { PR r; r.committed = committed; return r; }
 
-// Nesting limit of the parser (groups, bracket negations): the recursive descent below,
+// Nesting limit of the parser (groups, bracket negations; an alternation's '|' chain is a
+// loop and does not count): the recursive descent below,
 // like the reference's combine parser, takes stack per level, so a hostile pattern could
 // exhaust the caller's stack; past this depth the pattern is refused (FR_ERR_INVALID, a
 // limit of this build: the reference would overflow its stack instead).
 constexpr int MAX_NEST = 512;
+// Depth limit of the syntax tree itself (every consumer -- enumerator, recorder, merged
+// engine, printer -- walks it recursively): an alternation of n terms is an Either chain of
+// depth n, so flat alternations up to ~4,000 terms are taken (the group limit above does
+// not count them); deeper trees are refused with FR_ERR_INVALID, a limit of this build.
+constexpr size_t MAX_AST_DEPTH = 4096;
 
 struct Parser {
     const std::string& s;
@@ -162,20 +193,42 @@ struct Parser {
     PR regex(size_t i) {
         return memo(m_regex, h_regex, i, [&] { return regex_(i); });
     }
+    // The right recursion runs as a loop, so an alternation of any length takes no stack
+    // per alternative (only groups and bracket negations count as nesting):
+    // t_k = term(p_k), p_(k+1) = t_k.pos + 1 while t_k is followed by '|'; then from the
+    // last alternative back, regex(p_k) = Either(t_k, regex(p_(k+1))) if that succeeded,
+    // else t_k (attempt() restores the position: the '|' is left unconsumed).
     PR regex_(size_t i) {
-        Nest nest(depth);
-        PR t = term(i);
-        if (t.ok && at(t.pos, '|')) {
-            PR r = regex(t.pos + 1);
+        std::vector<size_t> ps{i};
+        std::vector<PR> ts;
+        for (;;) {
+            const size_t p = ps.back();
+            if (ps.size() > 1 && p < h_regex.size() && h_regex[p]) break;  // regex(p) already known
+            ts.push_back(term(p));
+            const PR& t = ts.back();
+            if (!(t.ok && at(t.pos, '|'))) break;
+            ps.push_back(t.pos + 1);
+        }
+        // r = regex(ps[K]) for the last position reached
+        size_t K = ps.size() - 1;
+        PR r = ts.size() == ps.size() ? ts.back() : m_regex[ps[K]];
+        if (ts.size() == ps.size()) {
+            if (ps[K] < h_regex.size()) m_regex[ps[K]] = r, h_regex[ps[K]] = 1;
+        }
+        for (size_t k = K; k-- > 0;) {
+            const PR& t = ts[k];
             if (r.ok) {
                 auto e = mk(Re::EITHER);
                 auto m = std::const_pointer_cast<Re>(e);
                 m->a = t.node;
                 m->b = r.node;
-                return ok(e, r.pos);
+                r = ok(e, r.pos);
+            } else {
+                r = t;
             }
+            if (k > 0 && ps[k] < h_regex.size()) m_regex[ps[k]] = r, h_regex[ps[k]] = 1;
         }
-        return term(i);
+        return r;
     }
     // term := many(factor); one factor is returned unwrapped (parser.rs:224-236)
     PR term(size_t i) {
@@ -239,6 +292,7 @@ struct Parser {
             return ok(x.node, x.pos + 1);
         }
         if (at(i, '(')) {
+            Nest nest(depth);
             PR r = regex(i + 1);
             if (!r.ok) return fail(true);
             if (!at(r.pos, ')')) return fail(true);
@@ -390,6 +444,9 @@ ReP parse(const std::string& pattern, int grammar) {
     bool ci = false;
     if (ps.at(i, 'i')) { ci = true; ++i; }
     ReP re = r.node;
+    if (ast_depth(*re) > MAX_AST_DEPTH)
+        throw Error(FR_ERR_INVALID, "pattern's syntax tree is deeper than " + std::to_string(MAX_AST_DEPTH) +
+                                        " levels (each alternative of an alternation is one level)");
     if (sof || eof) {
         auto q = std::make_shared<Re>();
         q->kind = Re::SEQ;
@@ -740,7 +797,8 @@ Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, s
 
 // ------------------------------------------------------------ enumeration cost
 namespace {
-struct DryPanic {};  // the enumeration would panic here: no count
+struct DryPanic {};   // the enumeration would panic here: no count
+struct DryMemory {};  // the counter's memo reached its byte bound: no count
 struct DryRes {
     std::vector<std::pair<size_t, uint64_t>> ends;  // (end position, multiplicity), ascending
     uint64_t spent = 0;                             // spend() total of one call
@@ -751,7 +809,11 @@ struct DryRes {
 struct Dry {
     size_t L;
     uint64_t cap;
+    uint64_t mem_cap;  // bound on the memo's bytes (entries + their stored end positions)
     std::map<std::pair<const Re*, size_t>, DryRes> memo;  // node references stay valid
+    uint64_t bytes = 0;
+    // a memo entry: the map node (key, DryRes, links) plus 16 B per (end, multiplicity)
+    static constexpr uint64_t ENTRY_BYTES = 96, END_BYTES = 16;
 
     uint64_t add(uint64_t a, uint64_t b) const { return a >= cap || b >= cap || a + b >= cap ? cap : a + b; }
     uint64_t mul(uint64_t a, uint64_t b) const {
@@ -789,10 +851,12 @@ struct Dry {
         const auto key = std::make_pair(re, p);
         auto it = memo.find(key);
         if (it != memo.end()) return it->second;
-        // a huge AST x content: no count (the caller enumerates, as before) rather than a
-        // memo of unbounded size
-        if (memo.size() >= ((size_t)1 << 20)) throw DryPanic{};
         DryRes r = compute(re, p);
+        // a huge AST x content: no count (the caller enumerates under its own budget, as
+        // without the counter) rather than a memo of unbounded size.  Every entry holds up
+        // to L - p + 1 end positions, so the bound is on bytes, not entries.
+        bytes += ENTRY_BYTES + END_BYTES * r.ends.size();
+        if (bytes > mem_cap) throw DryMemory{};
         return memo.emplace(key, std::move(r)).first->second;
     }
     DryRes compute(const Re* re, size_t p) {
@@ -834,7 +898,8 @@ struct Dry {
                 const DryRes& r0 = bb(re->xs[0].get(), p);
                 uint64_t spent = r0.spent;
                 std::map<size_t, uint64_t> conts = as_map(r0);
-                for (size_t i = 1; i < re->xs.size(); ++i) {
+                // once saturated the count is past cap whatever follows (as Repeated below)
+                for (size_t i = 1; i < re->xs.size() && spent < cap; ++i) {
                     conts = extend(conts, re->xs[i].get(), &spent);
                     spent = add(spent, total(conts));
                 }
@@ -892,9 +957,10 @@ uint64_t enumeration_spent(size_t L, const ReP& re, size_t lo, size_t hi, uint64
     return spent;
 }
 
-bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost) {
+CostOutcome enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost,
+                             uint64_t mem_bytes) {
     if (hi > L) hi = L;
-    Dry d{L, cap == UINT64_MAX ? cap : cap + 1, {}};
+    Dry d{L, cap == UINT64_MAX ? cap : cap + 1, mem_bytes ? mem_bytes : ENUM_COST_MEM_BYTES, {}};
     uint64_t t = 0;
     try {
         for (size_t i = lo; i < hi && t < d.cap; ++i) {  // record_has_match: spend(bs.size()) per start
@@ -902,10 +968,12 @@ bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t ca
             t = d.add(t, d.add(r.spent, r.size));
         }
     } catch (const DryPanic&) {
-        return false;
+        return COST_PANIC;
+    } catch (const DryMemory&) {
+        return COST_MEMORY;
     }
     *cost = t;
-    return true;
+    return COST_COUNTED;
 }
 
 Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pattern, size_t lo, size_t hi,
@@ -916,7 +984,6 @@ Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pat
     // a few million variants, else the state-merging evaluator.  The enumeration's cost
     // is counted first (enumeration_cost, exact), so a pattern past the budget goes
     // straight to the merged evaluator instead of building 2^22 branches and dropping
-    // them (config 5 at 512 chars: ~1 s of host time per cold call)
     // them (config 5 at 512 chars: ~1 s of host time per cold call).  Small enumerations
     // (/abc/ x 256: 763 variants) are tried directly: counting costs about as much as them.
     constexpr size_t budget = (size_t)1 << 22, small = (size_t)1 << 12;
@@ -926,8 +993,11 @@ Recorded record_has_match_engine(ValueDag& dag, size_t L, const std::string& pat
         if (e.code != FR_ERR_OOM) throw;
     }
     {
-        uint64_t cost = 0;
-        if (enumeration_cost(L, parse(pattern), lo, hi, budget, &cost) && cost > budget)
+        // no count (a panic, or the counter's memo bound: FR_ENUM_COST_BYTES overrides it,
+        // tests only) -> the enumeration below decides under its budget, as without the counter
+        uint64_t cost = 0, mem = 0;
+        if (const char* ev = std::getenv("FR_ENUM_COST_BYTES")) mem = std::strtoull(ev, nullptr, 10);
+        if (enumeration_cost(L, parse(pattern), lo, hi, budget, &cost, mem) == COST_COUNTED && cost > budget)
             return record_has_match_merged(dag, L, pattern, lo, hi);
     }
     try {

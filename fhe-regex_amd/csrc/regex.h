@@ -166,11 +166,15 @@ Recorded record_has_match(ValueDag& dag, size_t L, const std::string& pattern, s
 // What record_has_match would spend of its branch budget (the variants it enumerates),
 // counted without building a branch: per (node, position) the multiset of end positions
 // with multiplicities and the spends of one call, memoised, so it is polynomial in L
-// where the enumeration is exponential.  Saturates just past cap.  Returns false (no
-// count) where the enumeration would panic (empty Seq, a repetition count the reference
-// cannot allocate) or past 2^20 memoised (node, position) pairs: the caller then enumerates,
-// which reproduces the error or the exact decision.
-bool enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost);
+// where the enumeration is exponential.  Saturates just past cap.  No count where the
+// enumeration would panic (COST_PANIC: empty Seq, a repetition count the reference cannot
+// allocate) or once the memo would hold more than mem_bytes (COST_MEMORY; 0: the default
+// ENUM_COST_MEM_BYTES; entries and their stored end positions are counted): the caller
+// then enumerates, which reproduces the error or the exact decision.
+enum CostOutcome { COST_COUNTED = 0, COST_PANIC = 1, COST_MEMORY = 2 };
+constexpr uint64_t ENUM_COST_MEM_BYTES = (uint64_t)256 << 20;
+CostOutcome enumeration_cost(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap, uint64_t* cost,
+                             uint64_t mem_bytes = 0);
 // The same by enumerating (test hook): the spends, or cap + 1 once past cap.
 uint64_t enumeration_spent(size_t L, const ReP& re, size_t lo, size_t hi, uint64_t cap);
 // State-merging evaluator (merged.cpp, beyond the reference): the same boolean,

@@ -150,7 +150,8 @@ _SIGS = {
                                           C.POINTER(C.c_size_t), C.POINTER(C.c_uint32), C.c_size_t,
                                           C.POINTER(C.c_size_t), C.POINTER(C.c_int32), C.POINTER(C.c_size_t)]),
     "fr_debug_enumeration_cost": (C.c_int, [C.c_char_p, C.c_int32, C.c_size_t, C.c_size_t, C.c_size_t, C.c_uint64,
-                                            C.c_int32, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]),
+                                            C.c_uint64, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_uint64),
+                                            C.POINTER(C.c_uint64)]),
     "fr_parse": (C.c_int, [C.c_char_p, C.c_char_p, C.c_size_t]),
     "fr_set_plan_cache": (C.c_int, [C.c_void_p, C.c_size_t]),
     "fr_set_plan_cache_slots": (C.c_int, [C.c_void_p, C.c_size_t]),
@@ -259,9 +260,15 @@ def default_params(k: Optional[int] = None, N: Optional[int] = None, ring: Optio
 
 def parse(pattern: str, grammar: int = GRAMMAR_REFERENCE) -> str:
     """Canonical AST string (parser.rs:146-185; GRAMMAR_EXT: the opt-in class extension)."""
-    buf = C.create_string_buffer(1 << 16)
-    _check(lib().fr_parse_ex(pattern.encode("latin-1"), grammar, buf, len(buf)))
-    return buf.value.decode()
+    size = 1 << 16
+    while True:
+        buf = C.create_string_buffer(size)
+        rc = lib().fr_parse_ex(pattern.encode("latin-1"), grammar, buf, len(buf))
+        if rc == ERR_INVALID and size < (1 << 28) and b"buffer too small" in lib().fr_last_error():
+            size <<= 2
+            continue
+        _check(rc)
+        return buf.value.decode()
 
 
 def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESHOLD,
@@ -278,15 +285,23 @@ def plain_match(content: bytes | str, pattern: str, lowering: int = LOWER_THRESH
     return r
 
 
+COST_COUNTED, COST_PANIC, COST_MEMORY = 0, 1, 2
+
+
 def enumeration_cost(pattern: str, n_chars: int, start_lo: int = 0, start_hi: Optional[int] = None,
-                     cap: int = 1 << 22, enumerate: bool = False, grammar: int = GRAMMAR_REFERENCE):
+                     cap: int = 1 << 22, enumerate: bool = False, grammar: int = GRAMMAR_REFERENCE,
+                     mem_bytes: int = 0, with_outcome: bool = False):
     """(counted, enumerated): the reference enumeration's variant count from the AST
-    (None where it would panic) and, if asked, by enumerating; both saturate at cap + 1"""
+    (None without a count: where it would panic, or past the counter's memo bound
+    mem_bytes, 0 = AUTO's) and, if asked, by enumerating; both saturate at cap + 1.
+    with_outcome: (outcome, counted, enumerated), outcome one of COST_*."""
     hi = n_chars if start_hi is None else start_hi
-    c, e = C.c_uint64(), C.c_uint64()
-    _check(lib().fr_debug_enumeration_cost(pattern.encode("latin-1"), grammar, n_chars, start_lo, hi, cap,
-                                           int(enumerate), C.byref(c), C.byref(e)))
-    return (None if c.value == 2**64 - 1 else c.value), (e.value if enumerate else None)
+    o, c, e = C.c_int32(), C.c_uint64(), C.c_uint64()
+    _check(lib().fr_debug_enumeration_cost(pattern.encode("latin-1"), grammar, n_chars, start_lo, hi, cap, mem_bytes,
+                                           int(enumerate), C.byref(o), C.byref(c), C.byref(e)))
+    counted = c.value if o.value == COST_COUNTED else None
+    enumerated = e.value if enumerate else None
+    return (o.value, counted, enumerated) if with_outcome else (counted, enumerated)
 
 
 def plain_match_parts(content: bytes | str, pattern: str, start_lo: int, start_hi: int, max_parts: int,

@@ -379,12 +379,19 @@ int fr_set_grammar(fr_ctx* ctx, int32_t grammar);
 int fr_parse_ex(const char* pattern, int32_t grammar, char* buf, size_t buflen);
 int fr_plain_match_g(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,
                      int32_t lowering, int32_t engine, int32_t grammar, fr_plain_result* out);
-/* FR_ENGINE_AUTO's decision (round 5): the variants the reference's enumeration would build
- * for starts [start_lo, start_hi) of n_chars -- *counted from the AST without building them
- * (UINT64_MAX where the enumeration would panic), *enumerated by running it (enumerated ==
- * 0: not run) -- each saturating at cap + 1.  AUTO enumerates iff the count is <= 2^22. */
+/* FR_ENGINE_AUTO's decision: the variants the reference's enumeration would build for
+ * starts [start_lo, start_hi) of n_chars -- *counted from the AST without building them,
+ * *enumerated by running it (enumerate != 0; else 0) -- each saturating at cap + 1.
+ * *outcome says whether there is a count: FR_COST_COUNTED; FR_COST_PANIC, where the
+ * enumeration would panic (engine.rs:189-190, or a repetition it cannot allocate);
+ * FR_COST_MEMORY, where the counter's memo would exceed mem_bytes (0: the bound AUTO uses,
+ * 256 MiB; entries and the end positions they store are counted).  Without a count *counted
+ * is 0 and AUTO enumerates under its budget, as it would without the counter.  AUTO goes
+ * straight to the merged engine iff the count is > 2^22. */
+enum { FR_COST_COUNTED = 0, FR_COST_PANIC = 1, FR_COST_MEMORY = 2 };
 int fr_debug_enumeration_cost(const char* pattern, int32_t grammar, size_t n_chars, size_t start_lo, size_t start_hi,
-                              uint64_t cap, int32_t enumerate, uint64_t* counted, uint64_t* enumerated);
+                              uint64_t cap, uint64_t mem_bytes, int32_t enumerate, int32_t* outcome,
+                              uint64_t* counted, uint64_t* enumerated);
 /* fr_plain_match_g of fr_has_match_parts' program: out->result_lowered is the OR of the
  * parts, parts[0..*n_parts) their plaintext values (room for max_parts). */
 int fr_plain_match_parts(const char* content, size_t len, const char* pattern, size_t start_lo, size_t start_hi,

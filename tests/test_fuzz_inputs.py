@@ -155,10 +155,70 @@ def check_parse(p):
 def test_parse_adversarial():
     for p in adversarial_patterns():
         check_parse(p)
-    deep = "/" + "(" * (NEST_LIMIT - 1) + "a" + ")" * (NEST_LIMIT - 1) + "/"  # + the top level: 512
+    deep = "/" + "(" * NEST_LIMIT + "a" + ")" * NEST_LIMIT + "/"  # groups are the nesting levels
     assert F.parse(deep) == "Char(97)"
     with pytest.raises(F.FheRegexError, match="nests deeper"):
-        F.parse("/" + "(" * NEST_LIMIT + "a" + ")" * NEST_LIMIT + "/")
+        F.parse("/" + "(" * (NEST_LIMIT + 1) + "a" + ")" * (NEST_LIMIT + 1) + "/")
+
+
+def _deep(fn, *args):
+    """run an oracle call on a thread with a 1 GiB stack: the oracle's combinator parser
+    and enumerator recurse a few Python frames per alternative"""
+    import threading
+    out = {}
+
+    def run():
+        try:
+            out["v"] = fn(*args)
+        except Exception as e:  # noqa: BLE001 - re-raised on the caller's thread
+            out["e"] = e
+
+    old = threading.stack_size(1 << 30)
+    try:
+        t = threading.Thread(target=run)
+        t.start()
+        t.join()
+    finally:
+        threading.stack_size(old)
+    if "e" in out:
+        raise out["e"]
+    return out["v"]
+
+
+@pytest.mark.parametrize("n_alt", [513, 2000, 4000])
+def test_long_flat_alternation_parses(n_alt):
+    """a flat alternation is not nesting: /w0|w1|...|wn/ parses to the oracle's right-nested
+    Either at any length (parser.rs:208-222; the reference's combine parser takes it too)"""
+    rng = random.Random(n_alt)
+    words = ["".join(rng.choice("abcxyz") for _ in range(rng.randint(1, 3))) for _ in range(n_alt)]
+    p = "/" + "|".join(words) + "/"
+    assert F.parse(p) == str(_deep(ro.parse, p))
+    # inside groups and anchors, with a failing last alternative ('|' then nothing parses)
+    q = "/^(" + "|".join(words[:600]) + ")+$/"
+    assert F.parse(q) == str(_deep(ro.parse, q))
+    bad = "/" + "|".join(words[:700]) + "|)/"
+    with pytest.raises(F.ParseError):
+        F.parse(bad)
+    with pytest.raises(ro.ParseError):
+        _deep(ro.parse, bad)
+
+
+def test_alternation_deeper_than_tree_limit_refused():
+    """past MAX_AST_DEPTH (4096) levels the syntax tree is refused with an error, not a crash"""
+    with pytest.raises(F.FheRegexError, match="deeper than 4096"):
+        F.parse("/" + "a|" * 20000 + "a/")
+
+
+def test_alternation_plain_match_vs_oracle():
+    """a 2,000-alternative pattern through the enumerator and the lowering: the plaintext
+    result equals the oracle's"""
+    rng = random.Random(7)
+    words = ["".join(rng.choice("abc") for _ in range(3)) for _ in range(2000)]
+    p = "/" + "|".join(words) + "/"
+    for c in ("zzzz", "zz" + words[1234] + "z", "cab"):
+        r = F.plain_match(c, p)
+        exp = _deep(ro.has_match, c, p).result
+        assert r.result_recorded == r.result_lowered == exp, c
 
 
 def test_parse_mutations_vs_oracle():

@@ -1015,6 +1015,30 @@ def test_match_parts_cached_and_uncached_bit_identical(gctx):
         gctx.release(h)
 
 
+def test_plan_cache_key_not_forged_by_pattern(gctx):
+    """A pattern whose text ends like a cache-key suffix ('|parts4', '|lane1') is a plain
+    pattern to the cache: after fr_has_match_parts("/abc/", 4) cached its plan,
+    fr_has_match on "/abc/|parts4" still parses (and fails: the reference's Err) instead of
+    replaying the parts plan into a one-handle buffer; "/abc|lane\\1/" is its own plan."""
+    rng = np.random.default_rng(90)
+    s = _printable(rng, 40)
+    s = s[:10] + "abc" + s[13:]
+    hs = gctx.upload_radix(gctx.encrypt_str(s, seed=91))
+    gctx.set_plan_cache(8)
+    outs, _ = gctx.has_match_parts(hs, "/abc/", 0, 40, 4)
+    assert 1 < len(outs) <= 4
+    for bad in ("/abc/|parts4", "/abc/|parts4|lane1"):
+        with pytest.raises(F.ParseError):
+            gctx.has_match(hs, bad, 0, 40)
+    for pat in ("/abc|lane\\1/", "/abc|parts\\4/"):  # valid alternations, checked against the oracle
+        o, st = gctx.has_match(hs, pat)
+        assert st.plan_cached == 0
+        assert gctx.decrypt_radix(gctx.download_radix(o)) == ro.has_match(s, pat).result == 1
+        gctx.release(o)
+    for h in hs + outs:
+        gctx.release(h)
+
+
 # ------------------------------------- start-offset shards across contexts
 @pytest.mark.parametrize("world", [2, 4])
 @pytest.mark.parametrize("where", ["boundary", "absent"])

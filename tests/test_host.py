@@ -253,6 +253,36 @@ def test_enumeration_cost_counts_exactly():
         assert F.enumeration_cost(p, L, enumerate=True) == (exp, exp), p
 
 
+def test_enumeration_cost_memory_bound(monkeypatch):
+    """the counter's memo is bounded in bytes (entries and their stored end positions), and
+    running out of it is its own outcome, distinct from "the enumeration would panic"; AUTO
+    then enumerates under its own budget and so still takes the reference's decision"""
+    pat, L = "/a*b*c*d*/", 300
+    o, c, _ = F.enumeration_cost(pat, L, with_outcome=True)
+    assert o == F.COST_COUNTED and c > 0
+    o, c, _ = F.enumeration_cost(pat, L, mem_bytes=64 << 10, with_outcome=True)
+    assert (o, c) == (F.COST_MEMORY, None)
+    o, c, _ = F.enumeration_cost("/|a/", 4, with_outcome=True)  # empty Seq: engine.rs:189-190 panics
+    assert (o, c) == (F.COST_PANIC, None)
+    # AUTO with the counter starved: the same decision, counters and result as with it
+    content = "xaabbcdyab"
+    ref = F.plain_match(content, "/a*b*c*d*/", engine=F.ENGINE_AUTO)
+    monkeypatch.setenv("FR_ENUM_COST_BYTES", str(64 << 10))
+    got = F.plain_match(content, "/a*b*c*d*/", engine=F.ENGINE_AUTO)
+    exp = ro.has_match(content, "/a*b*c*d*/")
+    assert (got.ct_ops, got.cache_hits, got.result_recorded) == (ref.ct_ops, ref.cache_hits, ref.result_recorded) \
+        == (exp.ct_ops, exp.cache_hits, exp.result)
+    # past the enumeration budget (config 5 on 40 chars, ~2^22+ variants): merged, as with a count
+    pat5 = "/^a{2,8}(bc|de)+[^xyz]$/"
+    c5 = ("aaa" + "bcde" * 20)[:39] + "f"
+    monkeypatch.setenv("FR_ENUM_COST_BYTES", "4096")
+    assert F.enumeration_cost(pat5, 40, mem_bytes=4096) == (None, None)
+    a = F.plain_match(c5, pat5, engine=F.ENGINE_AUTO)
+    m = F.plain_match(c5, pat5, engine=F.ENGINE_MERGED)
+    assert (a.result_recorded, a.ct_ops, a.pbs) == (m.result_recorded, m.ct_ops, m.pbs)
+    assert a.result_recorded == ro.has_match_reach(c5, pat5) == 1
+
+
 def test_auto_engine_skips_a_doomed_enumeration():
     """config 5 at its 512 chars: AUTO counts ~2^252 variants and goes straight to the
     merged evaluator (round 4 built 2^22 branches first: ~1 s of host time per cold call);
