@@ -266,6 +266,22 @@ def pmc_figures(params, path: str):
             "source": os.path.relpath(path, REPO), "stale": d.get("kernel_sha") != sha}
 
 
+def named_length_record(value, ms, L, named, M, world, strong, ok, strong_starts, steps):
+    """BASELINE's named length (W["chars"]: 256 for the metric, 1,024 for config 4) at this N:
+    `value` itself when its timed region is one match of that length (N = 1, or a strong
+    split), else the strong_starts record (N > 1 with weak start shards: the named length
+    split by start offsets); None when neither ran.  A 1 -> N scaling plot of the named
+    workload reads named_length.value; `value` at N > 1 may be weak (N x the chars)."""
+    if L == named and M == 1 and (world == 1 or strong):
+        return {"chars": L, "value": value, "ms_per_step": ms, "steps": steps, "results_ok_steps": bool(ok),
+                "source": "value"}
+    if strong_starts and "value" in strong_starts:
+        return {"chars": strong_starts["content_chars"], "value": strong_starts["value"],
+                "ms_per_step": strong_starts["ms_per_step"], "steps": strong_starts["steps"],
+                "results_ok_steps": strong_starts["results_ok_steps"], "source": "strong_starts"}
+    return None
+
+
 def north_star_hbm(per_shape):
     """north_star's ">= 50% HBM roofline on the external-product kernel", evaluated at the
     dominant launch shape (the most BR time in the timed region): the physical fraction
@@ -1202,6 +1218,12 @@ def main():
         "faithful": faithful,
         "faithful_tree": faithful_tree,
         "strong_starts": strong_starts,
+        # BASELINE's named length (256 chars for the metric) at this N, whatever `value`'s
+        # sharding: the field a 1 -> 8 GPU scaling plot of the named workload reads
+        "named_length": named_length_record(total_rot / elapsed, ms_per_step, L, W["chars"], M, world, strong,
+                                            starts_ok if starts_ok is not None else
+                                            (result == (expected if shard == "matches" else expected[:1])),
+                                            strong_starts, args.steps),
         "kernel_saturated": kernel,
         "latency_probe": probe,
         "cpu_baseline": cpu,

@@ -111,6 +111,8 @@ def lib():
         L.or_bsk_fourier.argtypes = [C.c_void_p, C.POINTER(C.c_double)]
         L.or_torus_of.restype = C.c_uint64
         L.or_torus_of.argtypes = [C.c_double]
+        L.or_blind_rotate_exact.argtypes = [C.POINTER(Params), u64p, u64p, C.POINTER(C.c_uint8), C.c_int, C.c_int,
+                                            C.c_size_t, u64p]
         L.or_num_threads.restype = C.c_int
         L.or_set_threads.argtypes = [C.c_int]
         _lib = L
@@ -255,6 +257,20 @@ class Oracle:
         out = np.zeros((len(luts), self.big + 1), dtype=np.uint64)
         a = np.ascontiguousarray(ks_lwe, dtype=np.uint64)
         lib().or_blind_rotate_multi(self._pk, ptr(a), flat, len(luts), int(direct), ptr(out))
+        return out
+
+    def blind_rotate_exact(self, ks_lwes: np.ndarray, luts, direct: int = 1) -> np.ndarray:
+        """The torus ring's unrolled ladder in exact u64 arithmetic (schoolbook negacyclic
+        products mod 2^64, no f64): ks_lwes (count, n+1); luts (count, n_out, 16) or
+        (count, 16) for direct jobs; returns (count, n_out, kN+1)."""
+        assert self.P.ring == RING_FFT and self.bsk is not None
+        a = np.ascontiguousarray(ks_lwes.reshape(-1, self.n + 1), dtype=np.uint64)
+        count = a.shape[0]
+        l = np.ascontiguousarray(np.asarray(luts, dtype=np.uint8).reshape(count, -1, 16))
+        n_out = 1 if direct else l.shape[1]
+        out = np.zeros((count, n_out, self.big + 1), dtype=np.uint64)
+        lib().or_blind_rotate_exact(C.byref(self.P), ptr(self.bsk), ptr(a), ptr(l, C.c_uint8), l.shape[1], int(direct),
+                                    count, ptr(out))
         return out
 
     def gates(self, gates, slots: np.ndarray) -> np.ndarray:

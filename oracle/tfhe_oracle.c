@@ -894,6 +894,127 @@ void or_blind_rotate(void* pk, const uint64_t* ks_lwe, const uint8_t lut[16], ui
     or_blind_rotate_multi(pk, ks_lwe, lut, 1, 1, out);
 }
 
+/* ------------------------------------------- exact blind rotation (torus)
+ * The torus ring's unrolled CMUX ladder (blind_rotate_torus above) restated in exact
+ * integer arithmetic, independently of the f64 FFT's operation sequence: the accumulator
+ * is u64 (torus 2^64), the gadget digit of a coefficient is its top 23 bits rounded
+ * (signed, |d| <= 2^22, the same rule as acc_digit on the exact value), and every
+ * negacyclic product digit x GGSW polynomial is a schoolbook product with wrapping u64
+ * arithmetic -- exact mod 2^64.  Per step (pair i, i+1, e = (a_i + a_j, a_i, a_j)):
+ *   acc_c += sum_r D_r * H_rc,   H_rc = sum_g (X^e_g - 1) G_g[r][c]
+ * which is sum_g (X^e_g - 1) (sum_r D_r G_g[r][c]) by distributivity (exact in Z_2^64[X]).
+ * The w-step, sample extraction and sign offset are those of blind_rotate_torus.  Test
+ * infrastructure: it pins the f64 ladder (and the device, bit-identical to it) to the exact
+ * external products within a stated phase bound (tests/test_exact_br.py). */
+/* out += D * H (negacyclic, mod 2^64); D signed with |D| < 2^32 */
+static void nega_mac_small(int N, const int64_t* D, const uint64_t* H, uint64_t* out) {
+    for (int j = 0; j < N; j++) {
+        int64_t d = D[j];
+        if (!d) continue;
+        const uint64_t m = (uint64_t)(d < 0 ? -d : d); /* < 2^32: two 32 x 32 products per term */
+        const int neg = d < 0;
+        uint64_t* o = out + j;
+        const int n1 = N - j;
+        for (int t = 0; t < n1; t++) {
+            const uint64_t h = H[t];
+            const uint64_t v = m * (uint32_t)h + ((m * (h >> 32)) << 32);
+            o[t] += neg ? (uint64_t)0 - v : v;
+        }
+        o = out - n1; /* X^N = -1: coefficient t + j - N */
+        for (int t = n1; t < N; t++) {
+            const uint64_t h = H[t];
+            const uint64_t v = m * (uint32_t)h + ((m * (h >> 32)) << 32);
+            o[t] -= neg ? (uint64_t)0 - v : v;
+        }
+    }
+}
+/* (X^e poly)[t], e in [0, 2N), negacyclic, mod 2^64 */
+static inline uint64_t rot_u64(const uint64_t* poly, int N, int t, int e) {
+    int s = t - e;
+    s %= 2 * N; if (s < 0) s += 2 * N;
+    return s < N ? poly[s] : (uint64_t)0 - poly[s - N];
+}
+static void blind_rotate_exact(const or_params* P, const uint64_t* bsk, const uint64_t* ks_lwe, const uint8_t* luts,
+                               int n_out, int direct, uint64_t* outs, uint64_t* glwe_out) {
+    const int k = P->k, N = P->N, n = P->n, log2N2 = ilog2(2 * N), B = P->pbs_base_log;
+    const size_t kp1 = (size_t)k + 1, big = (size_t)k * N;
+    uint64_t* acc = calloc(kp1 * N, 8);
+    uint64_t* nacc = malloc(8 * kp1 * N);
+    int64_t* D = malloc(8 * kp1 * N);
+    uint64_t* H = malloc(8 * kp1 * kp1 * N);
+    uint64_t* V = malloc(8 * (size_t)N);
+    const uint64_t delta = 1ULL << 59;
+    if (direct == 1) {
+        int box = N / 16, half = box / 2;
+        for (int j = 0; j < N; j++) {
+            int m = (j + half) / box;
+            V[j] = m < 16 ? (uint64_t)luts[m] * delta : (uint64_t)0 - (uint64_t)luts[0] * delta;
+        }
+    } else for (int j = 0; j < N; j++) V[j] = delta / 2;
+    uint32_t b = mod_switch(ks_lwe[n], log2N2);
+    for (int j = 0; j < N; j++) acc[(size_t)k * N + j] = rot_u64(V, N, j, (2 * N - (int)b) % (2 * N));
+    for (int i = 0; i < n; i += 2) {
+        uint32_t ai = mod_switch(ks_lwe[i], log2N2);
+        uint32_t aj = i + 1 < n ? mod_switch(ks_lwe[i + 1], log2N2) : 0;
+        if (ai == 0 && aj == 0) continue;
+        const int e[3] = {(int)((ai + aj) % (2u * (uint32_t)N)), (int)ai, (int)aj};
+        /* digits: round(v / 2^(64-B)) of the signed value v (ties away from zero; a tie is an
+         * exact half, which the f64 ladder's ties-to-even can only meet on the same value) */
+        for (size_t c = 0; c < kp1 * (size_t)N; c++) {
+            const int64_t v = (int64_t)acc[c];
+            const int sh = 64 - B;
+            D[c] = (int64_t)((v >> sh) + ((v >> (sh - 1)) & 1));
+        }
+        /* H_rc = sum_g (X^e_g - 1) G_g[r][c] */
+        for (size_t rc = 0; rc < kp1 * kp1; rc++) {
+            uint64_t* h = H + rc * N;
+            for (int t = 0; t < N; t++) h[t] = 0;
+            for (int g = 0; g < 3; g++) {
+                if (e[g] == 0) continue;
+                const uint64_t* G = bsk + (((size_t)(i / 2) * 3 + g) * kp1 * kp1 + rc) * N;
+                for (int t = 0; t < N; t++) h[t] += rot_u64(G, N, t, e[g]) - G[t];
+            }
+        }
+        memcpy(nacc, acc, 8 * kp1 * N);
+        for (size_t c = 0; c < kp1; c++)
+            for (size_t r = 0; r < kp1; r++) nega_mac_small(N, D + r * N, H + (r * kp1 + c) * N, nacc + c * N);
+        memcpy(acc, nacc, 8 * kp1 * N);
+    }
+    if (glwe_out) memcpy(glwe_out, acc, 8 * kp1 * N);
+    int32_t pos[17], d[17];
+    for (int f = 0; f < (direct ? 1 : n_out); f++) {
+        uint64_t* out = outs + (size_t)f * (big + 1);
+        int nt = direct ? 0 : or_lut_terms(N, luts + 16 * f, pos, d);
+        for (size_t c = 0; c <= (size_t)k; c++) {
+            const uint64_t* A = acc + c * N;
+            for (int t = 0; t < (c < (size_t)k ? N : 1); t++) {
+                int src0 = t == 0 ? 0 : N - t;
+                uint64_t a = 0;
+                if (direct) a = A[src0];
+                else for (int q = 0; q < nt; q++) {
+                    int src = src0 - pos[q];
+                    int64_t dd = d[q];
+                    if (src < 0) { src += N; dd = -dd; }
+                    a += (uint64_t)dd * A[src];
+                }
+                out[c * N + t] = t == 0 ? a : (uint64_t)0 - a;
+            }
+        }
+        if (direct == 2) out[big] += 1ULL << 58;
+    }
+    free(acc); free(nacc); free(D); free(H); free(V);
+}
+/* count independent exact blind rotations (OpenMP over them): ks_lwe count*(n+1), luts
+ * count*n_out*16, outs count*n_out*(kN+1) (direct: n_out = 1) */
+void or_blind_rotate_exact(const or_params* P, const uint64_t* bsk, const uint64_t* ks_lwe, const uint8_t* luts,
+                           int n_out, int direct, size_t count, uint64_t* outs) {
+    const size_t big = (size_t)P->k * P->N, no = direct ? 1 : (size_t)n_out;
+    #pragma omp parallel for schedule(dynamic, 1)
+    for (long q = 0; q < (long)count; q++)
+        blind_rotate_exact(P, bsk, ks_lwe + (size_t)q * (P->n + 1), luts + (size_t)q * no * 16, n_out, direct,
+                           outs + (size_t)q * no * (big + 1), NULL);
+}
+
 /* ------------------------------------------------------------------ gates */
 /* A rotation job: c = offset*2^58 + sum_i w_i * in_i (mod 2^64), then one
  * blind rotation and n_out LUT outputs (direct: 0 multi-value, 1 the LUT

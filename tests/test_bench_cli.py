@@ -84,6 +84,24 @@ def test_n_gt_1_defaults_measure_named_lengths():
     assert bench.resolve_mode(*bench.default_mode("metric", "", ""), 8, 1) == (False, "starts")
 
 
+def test_named_length_record():
+    """named_length: the named workload at this N, whatever `value`'s
+    sharding -- `value` itself for one match of the named length (N = 1, or a strong split),
+    the hoisted strong_starts record when `value` is weak start shards (N x the chars)"""
+    import bench
+    r = bench.named_length_record(1e5, 7.0, 256, 256, 1, 1, False, True, None, 20)
+    assert r == {"chars": 256, "value": 1e5, "ms_per_step": 7.0, "steps": 20, "results_ok_steps": True,
+                 "source": "value"}
+    assert bench.named_length_record(2e5, 7.5, 1024, 1024, 1, 2, True, True,
+                                     {"same_as_value": True, "note": ""}, 5)["source"] == "value"
+    ss = {"value": 1.4e5, "ms_per_step": 5.1, "steps": 5, "content_chars": 256, "results_ok_steps": True}
+    r = bench.named_length_record(8e5, 7.2, 2048, 256, 1, 8, False, True, ss, 5)
+    assert r == {"chars": 256, "value": 1.4e5, "ms_per_step": 5.1, "steps": 5, "results_ok_steps": True,
+                 "source": "strong_starts"}
+    assert bench.named_length_record(8e5, 7.2, 2048, 256, 1, 8, False, True, None, 5) is None
+    assert bench.named_length_record(8e5, 7.2, 256, 256, 8, 1, False, True, None, 5) is None  # M matches
+
+
 def test_nccl_device_guard():
     """Under nccl every local rank needs its own GPU (RCCL refuses two ranks on one
     device); gloo rehearsals may share one"""
@@ -130,6 +148,7 @@ def test_one_rank_rccl_group_pipeline():
     assert d["n_gpus"] == 1 and d["config"]["shard"] == "starts" and "RCCL" in d["config"]["parallelism"]
     assert d["results_ok_steps"] is True and d["result_decrypted"] == d["result_expected"] == [1]
     assert len(d["per_rank"]) == 1 and d["weak_matches"]["results_ok_ranks"] == 1
+    assert d["named_length"]["chars"] == 256 and d["named_length"]["value"] == d["value"]
 
 
 @pytest.mark.gpu
@@ -153,3 +172,5 @@ def test_two_gloo_ranks_config4_named_length(parts):
     assert d["config"]["start_parts"] == (parts or 8)
     assert len(d["per_rank"]) == 2 and d["strong_starts"] == {"same_as_value": True,
                                                               "note": d["strong_starts"]["note"]}
+    assert d["named_length"]["source"] == "value" and d["named_length"]["chars"] == 1024
+    assert d["named_length"]["value"] == d["value"] and d["named_length"]["results_ok_steps"] is True
