@@ -512,7 +512,7 @@ def main():
         return
     if not args.pmc:  # the newest round's PMC summary of this parameter point
         name = "pmc_summary.json" if args.params == "k1n2048" else f"pmc_summary_{args.params}.json"
-        cands = [os.path.join(REPO, "profiles", r, name) for r in ("r05", "r04", "r03")]
+        cands = [os.path.join(REPO, "profiles", r, name) for r in ("r06", "r05", "r04", "r03")]
         args.pmc = next((c for c in cands if os.path.exists(c)), cands[-1])
     if args.matches < 1:
         ap.error("--matches must be >= 1")

@@ -840,6 +840,19 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
         const int t0 = __builtin_amdgcn_readfirstlane((int)nxt[0]);
         for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, t0 < steps ? t0 : 0);
     }
+#if defined(FR_PRIO_HALF_LAT) || defined(FR_PRIO_HALF_PAIR)
+    // A/B experiment (MI355X_MICROARCH.md "Two waves per SIMD", item 4): the second half of an
+    // 8-wave workgroup (waves 4-7: polynomial 1) loses VALU arbitration to its older SIMD
+    // partner at every segment head; one static s_setprio for that half before the loop
+    if constexpr (LAT) {
+#ifdef FR_PRIO_HALF_LAT
+        if (B == 1 && tid >= NT / 2) __builtin_amdgcn_s_setprio(FR_PRIO_HALF_LAT);
+#endif
+#ifdef FR_PRIO_HALF_PAIR
+        if (B == 2 && tid >= NT / 2) __builtin_amdgcn_s_setprio(FR_PRIO_HALF_PAIR);
+#endif
+    }
+#endif
     for (int t = 0; t < steps; ++t) {
         if (idle(t)) continue;  // (uniform branch)
         FBR_STAMP(0);

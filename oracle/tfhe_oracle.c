@@ -11,15 +11,22 @@
  * published shortint PBS algorithm (KS-first order: keyswitch -> modulus
  * switch -> blind rotation -> sample extract) at the parameters decoded from
  * the reference fixture test_data/client_key (PARAM_MESSAGE_2_CARRY_2:
- * n=742, k=1, N=2048, PBS 2^23 x 1, KS 2^3 x 5, Delta = 2^59), with one
- * documented deviation shared with the GPU product: the GLWE/GGSW ring is
- * Z_Q[X]/(X^N+1) with Q = 998244353 * 1004535809 (~2^59.8, exact integer
- * NTTs per prime + CRT) instead of tfhe-rs's torus 2^64 with an f64 FFT;
- * sample-extracted LWEs are mapped back to the 2^64 torus by
- * x -> sum_i round(2^64 * u_i / p_i) (u_i = x * (Q/p_i)^-1 mod p_i, which is
- * round(x * 2^64 / Q) up to one unit) so every ciphertext that crosses the
- * boundary decrypts with the reference's client key and the tfhe-rs decoding
- * rule (shortint decrypt_message_and_carry).
+ * n=742, k=1, N=2048, PBS 2^23 x 1, KS 2^3 x 5, Delta = 2^59).  Two GLWE/GGSW
+ * rings, as in the product (fheregex.h FR_RING_*):
+ *  - the torus ring (default): the 2^64 torus with an f64 negacyclic FFT,
+ *    tfhe-rs's own arithmetic class (concrete-fft 0.1.0, reference
+ *    Cargo.lock:110-114), restated from the operation sequence specified in
+ *    the product's csrc/fft.h (floating point is not associative: bit-identity
+ *    needs the same sequence); and, independently of that sequence, the same
+ *    unrolled ladder in exact u64 arithmetic (blind_rotate_exact: schoolbook
+ *    negacyclic products mod 2^64), the yardstick the f64 ladder is held to
+ *    (tests/test_exact_br.py);
+ *  - the RNS ring: Z_Q[X]/(X^N+1) with Q = 998244353 * 1004535809 (~2^59.8,
+ *    exact integer NTTs per prime + CRT); sample-extracted LWEs are mapped back
+ *    to the 2^64 torus by x -> sum_i round(2^64 * u_i / p_i) (u_i = x * (Q/p_i)^-1
+ *    mod p_i, which is round(x * 2^64 / Q) up to one unit).
+ * Every ciphertext that crosses the boundary decrypts with the reference's
+ * client key and the tfhe-rs decoding rule (shortint decrypt_message_and_carry).
  *
  * Call sites in the reference this path replaces: src/regex/execution.rs:76,
  * 93,110,143,173,190 (smart_eq/gt/le/bitand/bitor/bitxor), trivial constants

@@ -20,6 +20,30 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+# tests/test_gpu.py's RNS point: word-for-word whole-match comparisons whose oracle side
+# (the CPU RNS ring) takes 10-100 s each; run with FR_TEST_RNS=1 (the full matrix,
+# profiles/r06/gpu_tests_rns_matrix.log), deselected (not skipped) otherwise
+RNS_HEAVY = {"test_match_words_fuzz_scale", "test_match_words_full_size_configs", "test_faithful_tree_fuzz_scale",
+             "test_faithful_tree_full_metric", "test_match_words_lowering_variants", "test_match_words_start_shards",
+             "test_match_parts_words_start_shards"}
+
+
+def pytest_collection_modifyitems(config, items):
+    if os.environ.get("FR_TEST_RNS") == "1":
+        return
+    keep, drop = [], []
+    for it in items:
+        cs = getattr(it, "callspec", None)
+        heavy = it.originalname in RNS_HEAVY if hasattr(it, "originalname") else False
+        if heavy and cs is not None and "rns" in cs.id.split("-"):
+            drop.append(it)
+        else:
+            keep.append(it)
+    if drop:
+        config.hook.pytest_deselected(items=drop)
+        items[:] = keep
+
+
 @pytest.fixture(scope="session")
 def key_blob():
     with open(os.path.join(GOLDEN, "client_key"), "rb") as f:

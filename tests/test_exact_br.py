@@ -178,14 +178,16 @@ SHAPES = [("latency", 24, {}), ("pair", 300, {}), ("throughput", 300, {"FR_FFT_P
           ("dual", 300, {"FR_FFT_DUAL": 1})]
 
 
+SHAPE_CASES = [((1, 2048), s) for s in SHAPES] + [((2, 1024), s) for s in SHAPES if s[0] in ("latency", "throughput")]
+
+
 @pytest.mark.gpu
-@pytest.mark.parametrize("shape", SHAPES, ids=[s[0] for s in SHAPES])
+@pytest.mark.parametrize("point,shape", SHAPE_CASES, indirect=["point"],
+                         ids=[f"k{p[0]}n{p[1]}-{s[0]}" for p, s in SHAPE_CASES])
 def test_device_one_step_against_exact(key_blob, oracle_fft, point, monkeypatch, shape):
-    """every launch shape, one-step ladders: each output word of the device within 2^44 of
-    the exact ladder's"""
+    """every launch shape (pair and dual: k = 1 geometries), one-step ladders: each output
+    word of the device within 2^44 of the exact ladder's"""
     name, count, env = shape
-    if point[0] != 1 and name in ("pair", "dual"):
-        pytest.skip("pair and dual shapes are k = 1 geometries")
     ctx = _ctx(key_blob, point, monkeypatch, **env)
     O = oracle_fft
     ks, luts = one_step_inputs(O, count, seed=10 + count)

@@ -300,6 +300,7 @@ def _shape_ctx(key_blob, point, monkeypatch, **env):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("point", [(1, 2048)], indirect=True, ids=["k1n2048"])  # a k = 1 geometry
 @pytest.mark.parametrize("count", [301, 512])
 def test_fft_pair_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, count):
     """The pair shape (k = 1: two bootstraps per workgroup sharing key loads, twiddles
@@ -307,8 +308,6 @@ def test_fft_pair_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, coun
     on sampled rows and against the one-bootstrap throughput shape on every row, with
     zero pairs in one bootstrap's coefficients but not its partner's (steps the pair
     runs for one of them only)."""
-    if point[0] != 1:
-        pytest.skip("the pair shape is the k = 1 latency geometry")
     pair = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_PAIR_BATCH=4096)
     tp = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_PAIR_BATCH=0)
     O = oracle_fft
@@ -324,6 +323,7 @@ def test_fft_pair_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, coun
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("point", [(1, 2048)], indirect=True, ids=["k1n2048"])  # a k = 1 geometry
 @pytest.mark.parametrize("count", [257, 512])
 def test_fft_dual_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, count):
     """The dual shape (FR_FFT_DUAL=1, k = 1: one bootstrap per 4-wave workgroup, both
@@ -331,8 +331,6 @@ def test_fft_dual_shape_bit_exact(key_blob, oracle_fft, point, monkeypatch, coun
     the oracle on sampled rows and against the pair shape on every row, including rows
     with runs of zero pairs; and a whole /abc/ x 256 match bit-identical to the pair
     shape's."""
-    if point[0] != 1:
-        pytest.skip("the dual shape is the k = 1 geometry")
     dual = _shape_ctx(key_blob, point, monkeypatch, FR_FFT_DUAL=1)
     pair = _shape_ctx(key_blob, point, monkeypatch)
     O = oracle_fft
