@@ -176,6 +176,11 @@ __device__ __forceinline__ void finv_phase(double2 (&x)[E], const double2* tw, i
 #ifndef FR_PAIR_CC
 #define FR_PAIR_CC 1
 #endif
+// latency shape: the MAC's key-only part and own-row product before the MAC barrier, the next
+// step's key prefetch with them (1), or all of the MAC after the barrier (0)
+#ifndef FR_MAC_EARLY
+#define FR_MAC_EARLY 0
+#endif
 // latency shape, k = 1: the lane's twiddles in registers (1) or read from LDS (0)
 #ifndef FR_LAT_TWR
 #define FR_LAT_TWR 1
@@ -941,6 +946,66 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
 #pragma unroll
             for (int m = 0; m < E; ++m) row_bl[b * BS + G::template at<XL>(G::template moff<LAST>(m))] = x[b][m];
 #endif
+        // FR_MAC_EARLY (latency shape): everything of the MAC that does not read the other
+        // polynomials -- slot factors, the key-only K_r and the own-row product D_P K_P -- runs
+        // between the row writes and the barrier (the writes' completion hides behind it), the
+        // key registers die there, so the next step's prefetch issues before the barrier too
+        // (its issue cost in the barrier's wait); after the barrier only the other rows' reads
+        // and one cmac each.  Every value's operation sequence is the one below: same bits.
+        constexpr bool MAC_EARLY = LAT && B == 1 && FR_MAC_EARLY;
+        if constexpr (MAC_EARLY) {
+            double kxr_e[E][K], kxi_e[E][K];
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                const double2 own = x[0][m];
+                const uint32_t sm = ((m & 1) << 1) | ((m >> 1) & 1);  // brv2(m & 3)
+                double cr[3], ci[3];
+#pragma unroll
+                for (int h = 1; h < 3; ++h)
+                    slot_factor(bre[0][h - 1][m >> 2], bim[0][h - 1][m >> 2], h == 1 ? ei[0] : ej[0], sm, cr[h], ci[h]);
+                fft::cmul(cr[1], ci[1], cr[2], ci[2], cr[0], ci[0]);
+                double kor, koi;
+#pragma unroll
+                for (int gg = 0; gg < 3; ++gg) {
+                    const double c1r = cr[gg] - 1.0, c1i = ci[gg];
+                    const double2 Bo = gv[gg][0][m];
+                    if (gg == 0) fft::cmul(Bo.x, Bo.y, c1r, c1i, kor, koi);
+                    else fft::cmac(Bo.x, Bo.y, c1r, c1i, kor, koi);
+#pragma unroll
+                    for (int q = 0; q < K; ++q) {
+                        const double2 Bx = gv[gg][1 + q][m];
+                        if (gg == 0) fft::cmul(Bx.x, Bx.y, c1r, c1i, kxr_e[m][q], kxi_e[m][q]);
+                        else fft::cmac(Bx.x, Bx.y, c1r, c1i, kxr_e[m][q], kxi_e[m][q]);
+                    }
+                }
+                double zr, zi;
+                fft::cmul(own.x, own.y, kor, koi, zr, zi);
+                x[0][m] = make_double2(zr, zi);
+            }
+            if constexpr (LATPF && FR_MAC_EARLY == 1) {  // the next step's key, into the registers just freed
+                const int tn = __builtin_amdgcn_readfirstlane((int)nxt[t + 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, tn < steps ? tn : t);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int m = 0; m < E; ++m) {
+                double zr = x[0][m].x, zi = x[0][m].y;
+#pragma unroll
+                for (int q = 0; q < K; ++q) {
+                    const double2 oth = orow_bl[q][G::template at<XL>(G::template moff<LAST>(m))];
+                    fft::cmac(oth.x, oth.y, kxr_e[m][q], kxi_e[m][q], zr, zi);
+                }
+                x[0][m] = make_double2(zr, zi);
+            }
+            if constexpr (LATPF && FR_MAC_EARLY == 2) {  // (2: the prefetch after the cross terms, as without)
+                const int tn = __builtin_amdgcn_readfirstlane((int)nxt[t + 1]);
+                __builtin_amdgcn_sched_barrier(0);
+                for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, tn < steps ? tn : t);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        } else {
         // throughput shapes: slot m's GGSW values, loaded one slot ahead (E = 8) or
         // at the top of the slot (E = 4, 128 VGPRs: the other workgroup hides the wait)
         constexpr bool AHEAD = !LAT && E == 8;
@@ -1031,6 +1096,7 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
             for (int gg = 0; gg < NPF; ++gg) load_ggsw(gg, tn < steps ? tn : t);
             __builtin_amdgcn_sched_barrier(0);
         }
+        }  // !MAC_EARLY
         FBR_STAMP(3);
         // 4. inverse FFT (times M; 1/M is in the key), accumulate, reduce mod 2^64
         finverse_from<M, E, LAST, LAT, TWR, B, BS>(x, irow, twr, tw, twc, tl);

@@ -1,0 +1,6 @@
+# FR_MAC_EARLY=2 (prefetch after the cross terms) A/B and bit-exactness
+set -o pipefail
+mkdir -p gpurun_out/r06j
+SIZES="1 16 254" timeout -k 10 600 bash tools/ab_libs.sh 3 fhe-regex_amd/build/exp/lib_base.so fhe-regex_amd/build/exp/lib_macearly2.so > gpurun_out/r06j/ab_macearly.log 2>&1 &&
+FHEREGEX_LIB=fhe-regex_amd/build/exp/lib_macearly2.so timeout -k 10 600 python -u -m pytest tests/test_fft.py tests/test_gpu.py tests/test_exact_br.py -m gpu -x -q --timeout 200 --timeout-method thread -k "blind_rotate or match_words_abc_64 or one_step or reference_vectors or pair_shape or config4_the" > gpurun_out/r06j/tests_macearly.log 2>&1
+tail -3 gpurun_out/r06j/tests_macearly.log; cat gpurun_out/r06j/ab_macearly.log
