@@ -158,3 +158,30 @@ def test_match_under_generated_key(kN):
     dev = ctx.dev_blind_rotate(ks, [lut])[0]
     assert (dev == O.blind_rotate(ks[0], lut)).all()
     assert int(O.decode16(dev)[0]) == lut[6]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kN", [(1, 2048), (2, 1024)], ids=["fft", "fft-k2n1024"])
+def test_device_keygen_and_encryption_under_generated_key(kN):
+    """ServerKey::new (engine.rs:252) on the device under a freshly generated client key gives
+    the host generator's key word for word, and encrypt_str on the device (ciphertext.rs:32-40)
+    the host encryption's words, as with the fixture key (tests/test_keygen.py,
+    tests/test_client.py)"""
+    k, N = kN
+    p = F.default_params(k=k, N=N)
+    dev = F.Context(device=0, params=p)
+    dev.gen_client_key(77)
+    dev.set_keygen(F.KEYGEN_DEVICE)
+    dev.gen_server_key(5)
+    host = F.Context(device=-1, params=p)
+    host.load_client_key(dev.serialize_client_key())
+    host.gen_server_key(5)
+    dk, db = dev.export_server_key()
+    hk, hb = host.export_server_key()
+    assert np.array_equal(dk, hk) and np.array_equal(db, hb)
+    s = "GPU-encrypted, generated key"
+    hs = dev.encrypt_upload_str(s, seed=9)
+    ref = host.encrypt_str(s, seed=9)
+    for i in range(len(s)):
+        assert np.array_equal(dev.download_radix(hs[i]), ref[i]), i
+        assert dev.decrypt_radix(ref[i]) == ord(s[i])
