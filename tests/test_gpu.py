@@ -227,6 +227,20 @@ def test_reference_vectors_encrypted_content(gctx, v):
         gctx.release(h)
 
 
+def test_readme_semantics_encrypted(gctx):
+    """The reference README's documented constructs (README.md:33-58, tests/golden/
+    readme_vectors.json: 100 pattern/content cases, the two ct_ge quirk cases following the
+    code) on encrypted content, each result decrypted"""
+    cases = load("readme_vectors.json")["cases"]
+    for i, c in enumerate(cases):
+        exp = c.get("code", c["readme"])
+        hs = gctx.encrypt_upload_str(c["content"], seed=500 + i) if c["content"] else []
+        out, _ = gctx.has_match(hs, c["pattern"])
+        assert gctx.decrypt_radix(gctx.download_radix(out)) == exp, c
+        for h in hs + [out]:
+            gctx.release(h)
+
+
 def test_eager_ops(gctx):
     s = "aMz~ 0"
     hs = gctx.upload_radix(gctx.encrypt_str(s, seed=9))

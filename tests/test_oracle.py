@@ -219,3 +219,24 @@ def test_reach_simulator_vs_enumerator_fuzz():
             got, g_exc = None, type(e).__name__
         assert (got, g_exc) == (exp, e_exc), (c, p)
         n += 1
+
+
+def test_readme_semantics_vectors():
+    """The reference README's documented semantics (README.md:33-58, transcribed by
+    tests/golden/make_readme_vectors.py): the oracle and the product's recorded and lowered
+    circuits (both engines) give the README's claim on every case, except the two where the
+    code itself differs (ct_ge calls smart_gt, execution.rs:93), which follow the code."""
+    import json
+    import fheregex as F
+    with open(os.path.join(GOLDEN, "readme_vectors.json")) as f:
+        cases = json.load(f)["cases"]
+    assert len(cases) == 100
+    quirks = 0
+    for c in cases:
+        exp = c.get("code", c["readme"])
+        quirks += "code" in c
+        assert ro.has_match(c["content"], c["pattern"]).result == exp, c
+        for eng in (F.ENGINE_ENUMERATE, F.ENGINE_MERGED):
+            r = F.plain_match(c["content"], c["pattern"], engine=eng)
+            assert (r.result_recorded, r.result_lowered) == (exp, exp), (c, eng)
+    assert quirks == 2
