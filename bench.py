@@ -478,6 +478,8 @@ def main():
                     help="gates in the CPU baseline sample (0: skip; 2048 ~ 10 s on 16 threads)")
     ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated throughput probe (0: skip)")
+    ap.add_argument("--saturate-iters", type=int, default=10,
+                    help="back-to-back launches the saturated probe times (after one warm-up launch)")
     ap.add_argument("--fresh-steps", type=int, default=5,
                     help="N=1: matches on newly encrypted content (encryption outside the timing; 0: skip)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -1054,10 +1056,11 @@ def main():
         src = [h for h in handles if h != F.NULL_CT]
         hs = [src[i % len(src)] for i in range(args.saturate)]
         ctx.dev_bench_pbs(hs, 1)  # warm-up, as the latency probe below
-        br_sat, tot_sat = ctx.dev_bench_pbs(hs, 2)
-        kernel = {"gates_per_launch": args.saturate, "br_ms_per_launch": br_sat / 2,
-                  "pbs_per_s": 2 * args.saturate / (tot_sat / 1e3),
-                  "br_pbs_per_s": 2 * args.saturate / (br_sat / 1e3)}
+        it = max(1, args.saturate_iters)
+        br_sat, tot_sat = ctx.dev_bench_pbs(hs, it)
+        kernel = {"gates_per_launch": args.saturate, "launches": it, "br_ms_per_launch": br_sat / it,
+                  "pbs_per_s": it * args.saturate / (tot_sat / 1e3),
+                  "br_pbs_per_s": it * args.saturate / (br_sat / 1e3)}
 
     probe = None
     if args.probe.strip("' ") and rank == 0:
