@@ -51,7 +51,10 @@ algorithmic f64 FLOP per bootstrap (algorithmic_flops_per_pbs) x bootstraps /
 BR time against the FP64 vector peak; the HBM side reports the physical traffic
 (rocprofv3 PMC of this kernel source, tools/profile.sh -> tools/pmc_summary.py)
 per launch time.  cpu_baseline: the CPU restatement (oracle/, "port") timed on
-this host's available cores.
+this host's available cores.  kernel_saturated: 2048 bootstraps per launch, 10 launches
+after a warm-up.  power: socket power and energy per bootstrap of rank 0's GPU over the
+timed region and the saturated probe (the driver's energy accumulator, read outside
+each region; --no-power skips it), against the board's power cap.
 """
 import argparse
 import hashlib
@@ -300,6 +303,46 @@ def north_star_hbm(per_shape):
                     "algorithmic figure is not a physical rate (it exceeds 1.0 at >= 512 bootstraps per launch)"}
 
 
+class EnergyMeter:
+    """Socket energy of this rank's GPU from the driver's energy accumulator (amdsmi; no HIP),
+    read outside the timed regions: average power and energy per bootstrap of a region, and the
+    board's power cap (tools/power_probe.py samples the same table every 4 ms).  Any failure
+    (no amdsmi, no permission, no matching device) leaves the meter off: the records are null."""
+
+    def __init__(self, torch_props):
+        self.h = None
+        self.cap_w = None
+        try:
+            import amdsmi
+
+            amdsmi.amdsmi_init()
+            want = (torch_props.pci_domain_id, torch_props.pci_bus_id, torch_props.pci_device_id)
+            for h in amdsmi.amdsmi_get_processor_handles():
+                dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
+                if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
+                    self.h = h
+            if self.h is not None:
+                self.amdsmi = amdsmi
+                self.cap_w = amdsmi.amdsmi_get_power_cap_info(self.h)["power_cap"] / 1e6
+        except Exception:  # noqa: BLE001 -- the meter is an extra, never a failure of the bench
+            self.h = None
+
+    def read(self):
+        if self.h is None:
+            return None
+        try:
+            e = self.amdsmi.amdsmi_get_energy_count(self.h)
+            return e["energy_accumulator"] * e["counter_resolution"] * 1e-6, time.perf_counter()
+        except Exception:  # noqa: BLE001
+            return None
+
+    def region(self, r0, r1, bootstraps):
+        if r0 is None or r1 is None or r1[1] <= r0[1] or r1[0] < r0[0]:
+            return None
+        j, s = r1[0] - r0[0], r1[1] - r0[1]
+        return {"w": j / s, "seconds": s, "mj_per_bootstrap": 1e3 * j / bootstraps if bootstraps else None}
+
+
 def free_port() -> int:
     import socket
 
@@ -478,6 +521,7 @@ def main():
                     help="gates in the CPU baseline sample (0: skip; 2048 ~ 10 s on 16 threads)")
     ap.add_argument("--cpu-match-max-jobs", type=int, default=2000, help="largest schedule the CPU match runs")
     ap.add_argument("--saturate", type=int, default=2048, help="gates in the saturated throughput probe (0: skip)")
+    ap.add_argument("--no-power", action="store_true", help="no energy-accumulator readings (amdsmi) around the timed regions")
     ap.add_argument("--saturate-iters", type=int, default=10,
                     help="back-to-back launches the saturated probe times (after one warm-up launch)")
     ap.add_argument("--fresh-steps", type=int, default=5,
@@ -761,9 +805,11 @@ def main():
         for h in o:
             ctx.release(h)
 
+    meter = EnergyMeter(torch.cuda.get_device_properties(device)) if rank == 0 and not args.no_power else None
     ctx.set_profiling(True)
     t_before = ctx.device_timers()
     barrier()
+    e_timed0 = meter.read() if meter else None
     t0 = time.perf_counter()
     rot_local = 0
     host_ms = 0.0
@@ -783,6 +829,7 @@ def main():
             outs = o
     barrier()
     elapsed = time.perf_counter() - t0
+    e_timed1 = meter.read() if meter else None
     t_after = ctx.device_timers()
     ctx.set_profiling(False)
     ms_per_step_local = elapsed / args.steps * 1e3
@@ -1052,12 +1099,15 @@ def main():
                                             "`value`)")
 
     kernel = None
+    e_sat0 = e_sat1 = None
     if args.saturate and rank == 0:
         src = [h for h in handles if h != F.NULL_CT]
         hs = [src[i % len(src)] for i in range(args.saturate)]
         ctx.dev_bench_pbs(hs, 1)  # warm-up, as the latency probe below
         it = max(1, args.saturate_iters)
+        e_sat0 = meter.read() if meter else None
         br_sat, tot_sat = ctx.dev_bench_pbs(hs, it)
+        e_sat1 = meter.read() if meter else None
         kernel = {"gates_per_launch": args.saturate, "launches": it, "br_ms_per_launch": br_sat / it,
                   "pbs_per_s": it * args.saturate / (tot_sat / 1e3),
                   "br_pbs_per_s": it * args.saturate / (br_sat / 1e3)}
@@ -1228,6 +1278,14 @@ def main():
                                             (result == (expected if shard == "matches" else expected[:1])),
                                             strong_starts, args.steps),
         "kernel_saturated": kernel,
+        # socket power and energy per bootstrap of rank 0's GPU (driver energy accumulator) over the
+        # timed region and the saturated probe; the board's power cap bounds the saturated rate
+        "power": None if meter is None or meter.h is None else {
+            "source": "amdsmi energy accumulator (socket), read outside each region; rank 0's GPU",
+            "cap_w": meter.cap_w,
+            "timed_region": meter.region(e_timed0, e_timed1, rot_local),
+            "saturated": meter.region(e_sat0, e_sat1, kernel["launches"] * kernel["gates_per_launch"]) if kernel else None,
+        },
         "latency_probe": probe,
         "cpu_baseline": cpu,
     }

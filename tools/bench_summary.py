@@ -18,7 +18,7 @@ def main(path):
             if v:
                 print(f"  {k}: launches={v['launches']} per_launch={v['bootstraps_per_launch']:.0f} "
                       f"avg_ms={v['avg_ms']:.3f} frac={v['frac']:.3f}")
-    for key in ("latency_probe", "kernel_saturated", "fresh_content", "faithful", "faithful_tree", "inflight", "inflight_1ctx",
+    for key in ("latency_probe", "kernel_saturated", "power", "fresh_content", "faithful", "faithful_tree", "inflight", "inflight_1ctx",
                 "strong_starts", "weak_matches", "step_latency"):
         v = d.get(key)
         if v:
