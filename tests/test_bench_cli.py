@@ -102,6 +102,21 @@ def test_named_length_record():
     assert bench.named_length_record(8e5, 7.2, 256, 256, 8, 1, False, True, None, 5) is None  # M matches
 
 
+def test_energy_meter_off_without_gpu():
+    """the power record's meter: off (never an error) when amdsmi finds no matching GPU, as here;
+    a region is watts = joules / seconds and mJ per bootstrap, null on a counter that went back"""
+    import types
+
+    import bench
+    props = types.SimpleNamespace(pci_domain_id=0, pci_bus_id=0x72, pci_device_id=0)
+    m = bench.EnergyMeter(props)
+    assert m.h is None and m.read() is None
+    assert m.region((100.0, 1.0), (112.5, 1.01), 2048) == pytest.approx(
+        {"w": 1250.0, "seconds": 0.01, "mj_per_bootstrap": 12.5e3 / 2048})
+    assert m.region((100.0, 1.0), (99.0, 1.01), 10) is None
+    assert m.region(None, (1.0, 1.0), 10) is None
+
+
 def test_nccl_device_guard():
     """Under nccl every local rank needs its own GPU (RCCL refuses two ranks on one
     device); gloo rehearsals may share one"""
