@@ -918,6 +918,22 @@ int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* b
     })
 }
 
+int fr_load_server_key(fr_ctx* ctx, const uint64_t* ksk, size_t ksk_len, const uint64_t* bsk, size_t bsk_len) {
+    FR_TRY({
+        NEED(ctx && ksk && bsk);
+        const Params& p = ctx->p;
+        if (ksk_len != (size_t)p.big() * p.ks_level * (p.n + 1) || bsk_len != p.bsk_len())
+            throw Error(FR_ERR_INVALID, "server key lengths do not match the context params (fr_server_key_sizes)");
+        ctx->has_sk = false;
+        std::vector<uint64_t> k(ksk, ksk + ksk_len), b(bsk, bsk + bsk_len);
+        if (ctx->dev) ctx->dev->upload_keys(k, b);
+        ctx->ksk = std::move(k);
+        ctx->bsk = std::move(b);
+        ctx->sk_on_device = false;
+        ctx->has_sk = true;
+    })
+}
+
 int fr_encrypt_blocks(fr_ctx* ctx, const uint8_t* msgs, size_t count, uint64_t seed, uint64_t first_block,
                       uint64_t* out) {
     FR_TRY({

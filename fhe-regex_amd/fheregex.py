@@ -113,6 +113,7 @@ _SIGS = {
     "fr_set_keygen": (C.c_int, [C.c_void_p, C.c_int32]),
     "fr_export_server_key": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
     "fr_server_key_sizes": (C.c_int, [C.c_void_p, C.POINTER(C.c_size_t), C.POINTER(C.c_size_t)]),
+    "fr_load_server_key": (C.c_int, [C.c_void_p, u64p, C.c_size_t, u64p, C.c_size_t]),
     "fr_encrypt_str": (C.c_int, [C.c_void_p, C.c_char_p, C.c_size_t, C.c_uint64, u64p]),
     "fr_encrypt_blocks": (C.c_int, [C.c_void_p, C.POINTER(C.c_uint8), C.c_size_t, C.c_uint64, C.c_uint64, u64p]),
     "fr_decrypt_radix": (C.c_int, [C.c_void_p, u64p, u64p]),
@@ -381,6 +382,13 @@ class Context:
         bsk = np.zeros(b.value, dtype=np.uint64)
         _check(lib().fr_export_server_key(self.h, _p(ksk), len(ksk), _p(bsk), len(bsk)))
         return ksk, bsk
+
+    def load_server_key(self, ksk: np.ndarray, bsk: np.ndarray):
+        """install an exported server key (export_server_key's arrays): a server context
+        holding only sk, as has_match(sk, ...) takes it (engine.rs:8); no client key needed"""
+        k = np.ascontiguousarray(ksk, dtype=np.uint64)
+        b = np.ascontiguousarray(bsk, dtype=np.uint64)
+        _check(lib().fr_load_server_key(self.h, _p(k), len(k), _p(b), len(b)))
 
     def set_lowering(self, mode: int):
         _check(lib().fr_set_lowering(self.h, mode))

@@ -20,6 +20,8 @@
  *                                                     fr_load_client_key + fr_gen_server_key
  *   engine.rs:238-246 generate_test_keys: bincode::serialize(client key)
  *                                                     fr_serialize_client_key
+ *   engine.rs:8 has_match(sk, ...): a server holding only sk
+ *                                                     fr_export_server_key -> fr_load_server_key
  *   ciphertext.rs:32-40 encrypt_str / RadixClientKey::encrypt
  *                                                     fr_encrypt_str (client side, test/bench)
  *   mod.rs:17 / engine.rs:289 RadixClientKey::decrypt fr_decrypt_radix (client side)
@@ -140,6 +142,14 @@ int fr_set_keygen(fr_ctx* ctx, int32_t where);
  * fr_server_key_sizes.  Either may be NULL. */
 int fr_export_server_key(fr_ctx* ctx, uint64_t* ksk, size_t ksk_len, uint64_t* bsk, size_t bsk_len);
 int fr_server_key_sizes(fr_ctx* ctx, size_t* ksk_len, size_t* bsk_len);
+/* Install a server key in fr_export_server_key's layout: a server context that
+ * holds only `sk`, as has_match(sk, content, pattern) takes it (engine.rs:8), never
+ * the client key (the reference keeps both in one process: gen_keys, ciphertext.rs:42-45;
+ * ServerKey::new, engine.rs:252).  Needs no client key; any client key stays.  The
+ * device transforms the BSK into its ring's domain as after fr_gen_server_key.  Lengths
+ * other than fr_server_key_sizes' -> FR_ERR_INVALID.  This is the build's own layout,
+ * not tfhe-rs's bincode ServerKey. */
+int fr_load_server_key(fr_ctx* ctx, const uint64_t* ksk, size_t ksk_len, const uint64_t* bsk, size_t bsk_len);
 
 /* ----- client side (tests / bench; not on the timed path) ----- */
 int fr_encrypt_str(fr_ctx* ctx, const char* s, size_t len, uint64_t seed, uint64_t* out /* len*4*(kN+1) */);

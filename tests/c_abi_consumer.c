@@ -93,6 +93,27 @@ int main(int argc, char** argv) {
         }
         free(back);
         free(blob);
+        /* a server holding only the exported server key (has_match(sk, ..), engine.rs:8) */
+        size_t kl = 0, bl = 0;
+        CHECK(fr_gen_server_key(ctx, 42) == FR_OK, "host server key: %s", fr_last_error());
+        CHECK(fr_server_key_sizes(ctx, &kl, &bl) == FR_OK && kl && bl, "server key sizes");
+        uint64_t* ksk = (uint64_t*)malloc(8 * kl);
+        uint64_t* bsk = (uint64_t*)malloc(8 * bl);
+        uint64_t* bsk2 = (uint64_t*)malloc(8 * bl);
+        fr_ctx* srv = NULL;
+        CHECK(fr_ctx_create(&p, -1, &srv) == FR_OK && srv, "server context");
+        if (ksk && bsk && bsk2 && srv) {
+            CHECK(fr_export_server_key(ctx, ksk, kl, bsk, bl) == FR_OK, "export: %s", fr_last_error());
+            CHECK(fr_load_server_key(srv, ksk, kl, bsk, bl - 1) == FR_ERR_INVALID, "short bsk refused");
+            CHECK(fr_load_server_key(srv, ksk, kl, bsk, bl) == FR_OK, "load server key: %s", fr_last_error());
+            CHECK(fr_export_server_key(srv, NULL, 0, bsk2, bl) == FR_OK && memcmp(bsk, bsk2, 8 * bl) == 0,
+                  "export(load(k)) == k");
+            CHECK(fr_serialize_client_key(srv, NULL, 0, &need) == FR_ERR_NO_KEY, "the server has no client key");
+        }
+        if (srv) fr_ctx_destroy(srv);
+        free(ksk);
+        free(bsk);
+        free(bsk2);
         fr_ct content[1] = {0};
         fr_ct out = 0;
         CHECK(fr_has_match(ctx, content, 1, "/a/", &out, NULL) == FR_ERR_NO_DEVICE, "has_match needs a device");
