@@ -691,6 +691,19 @@ class ServerKey:
     def create_trivial_radix(self, msg: int) -> int:
         return self.ctx.trivial(msg)
 
+    def save(self, path: str):
+        """the server key as an .npz of its (ksk, bsk) arrays (fr_export_server_key's layout)"""
+        ksk, bsk = self.ctx.export_server_key()
+        np.savez(path, ksk=ksk, bsk=bsk)
+
+    @staticmethod
+    def load(path: str, device: int = 0, params: Optional[Params] = None) -> "ServerKey":
+        """a server context holding only this server key (fr_load_server_key; no client key)"""
+        ctx = Context(device, params)
+        with np.load(path, allow_pickle=False) as z:
+            ctx.load_server_key(z["ksk"], z["bsk"])
+        return ServerKey(ctx)
+
 
 def gen_keys(client_key_blob: Optional[bytes] = None, seed: int = 0, device: int = 0,
              params: Optional[Params] = None, client_seed: Optional[int] = None):

@@ -39,6 +39,16 @@ def test_load_server_key_roundtrip_host(host_client):
         server.serialize_client_key()  # the server never saw a client key
 
 
+def test_server_key_file_roundtrip(host_client, tmp_path):
+    """ServerKey.save / ServerKey.load: the arrays through an .npz (no pickle)"""
+    path = str(tmp_path / "sk.npz")
+    F.ServerKey(host_client).save(path)
+    sk = F.ServerKey.load(path, device=-1)
+    a, b = host_client.export_server_key()
+    a2, b2 = sk.ctx.export_server_key()
+    assert np.array_equal(a, a2) and np.array_equal(b, b2)
+
+
 def test_load_server_key_wrong_lengths(host_client):
     ksk, bsk = host_client.export_server_key()
     server = F.Context(device=-1)
