@@ -321,6 +321,9 @@ class EnergyMeter:
                 dom, bus, rest = amdsmi.amdsmi_get_gpu_device_bdf(h).split(":")
                 if (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16)) == want:
                     self.h = h
+            import atexit
+
+            atexit.register(amdsmi.amdsmi_shut_down)
             if self.h is not None:
                 self.amdsmi = amdsmi
                 self.cap_w = amdsmi.amdsmi_get_power_cap_info(self.h)["power_cap"] / 1e6
