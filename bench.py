@@ -1286,7 +1286,9 @@ def main():
         "power": None if meter is None or meter.h is None else {
             "source": "amdsmi energy accumulator (socket), read outside each region; rank 0's GPU",
             "cap_w": meter.cap_w,
-            "timed_region": meter.region(e_timed0, e_timed1, rot_local),
+            # ranks sharing one GPU (gloo rehearsals): the socket's energy is every rank's work
+            "timed_region": meter.region(e_timed0, e_timed1,
+                                         rot_local if world <= torch.cuda.device_count() else None),
             "saturated": meter.region(e_sat0, e_sat1, kernel["launches"] * kernel["gates_per_launch"]) if kernel else None,
         },
         "latency_probe": probe,
