@@ -1619,6 +1619,8 @@ void Device::build_ksk_limbs() {
 void Device::upload_keys(const std::vector<uint64_t>& ksk, const std::vector<uint64_t>& bsk) {
     if (ksk.size() != (size_t)p_.big() * p_.ks_level * (p_.n + 1)) throw Error(FR_ERR_INVALID, "ksk size");
     if (bsk.size() != p_.bsk_len()) throw Error(FR_ERR_INVALID, "bsk size");
+    // every queued launch of every lane that reads the old keys has finished before they go
+    HIP_CHECK(hipDeviceSynchronize());
     (void)hipFree(d_ksk_);
     (void)hipFree(d_bsk_);
     d_ksk_ = nullptr;

@@ -259,6 +259,8 @@ void Device::gen_server_key(const ClientKey& ck, uint64_t seed) {
     const int N = p_.N, M = N / 2, kp1 = p_.k + 1, n = p_.n, L = p_.ks_level;
     const size_t rows = (size_t)p_.big() * L, nw = p_.bsk_ggsw();
     const size_t bsk_polys = nw * kp1 * kp1;
+    // every queued launch of every lane that reads the old keys has finished before they go
+    KG_CHECK(hipDeviceSynchronize());
     // host: the noise draws and per-GGSW messages
     std::vector<int64_t> ksk_noise;
     std::vector<int32_t> bsk_noise;

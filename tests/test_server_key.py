@@ -94,3 +94,8 @@ def test_server_without_client_key(point, key_blob):
         ref_out, _ = both.has_match(both.upload_radix(ct), "/abc/")
         assert np.array_equal(both.download_radix(ref_out), words)
         assert st.blind_rotations > 0
+        # a key installed while a match is still queued (calls are asynchronous): the device
+        # drains before the old key's buffers go, and the queued match reads the old key
+        queued, _ = server.has_match(server.upload_radix(ct), "/abc/")
+        server.load_server_key(ksk, bsk)
+        assert np.array_equal(server.download_radix(queued), words)
