@@ -240,6 +240,19 @@ def cpu_baseline(params, content: bytes, pattern: str, grammar: int, engine: int
     }
 
 
+def kernel_source_sha():
+    """what the blind-rotation kernels are compiled from: fft_br.hip, the pair shape's translation
+    unit and the Makefile that sets its scheduler (tools/pmc_summary.py hashes the same)"""
+    h = hashlib.sha256()
+    for rel in ("csrc/fft_br.hip", "csrc/fft_br_pair.hip", "Makefile"):
+        path = os.path.join(REPO, "fhe-regex_amd", rel)
+        if not os.path.exists(path):
+            return None
+        with open(path, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_figures(params, path: str):
     """traffic (HBM bytes per BR launch) and the VALU issue rate of the BR kernel
     from tools/pmc_summary.py's JSON; stale when the kernel source changed since."""
@@ -250,8 +263,7 @@ def pmc_figures(params, path: str):
         return None
     if d.get("ring", "rns") != ("fft" if params.ring == F.RING_FFT else "rns") or d.get("k", 1) != params.k:
         return None
-    src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
-    sha = hashlib.sha256(open(src, "rb").read()).hexdigest()[:16] if os.path.exists(src) else None
+    sha = kernel_source_sha()
     shapes = {}
     lns = d.get("launches", [])
     sat_grid = max((ln.get("grid", 0) for ln in lns), default=None)  # the saturated probe (as pmc_summary.py)

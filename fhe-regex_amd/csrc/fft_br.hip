@@ -1177,6 +1177,17 @@ k_blind_rotate_fft(const uint64_t* __restrict__ ks, int ks_stride, int n, const 
     }
 }
 
+// The pair shape's one instantiation is compiled in its own translation unit,
+// fft_br_pair.hip, under the max-ILP machine scheduler (Makefile: PAIR_SCHED).  A/B on one box
+// (profiles/r06/ab_sched.log): 512 / 2048 bootstraps 1.6% / 1.4% faster, while the latency shape
+// loses 6% under that scheduler and keeps the default here.  Scheduling does not change an
+// operation, so the results are the same bits.
+#ifndef FR_BR_PAIR_TU
+extern template __global__ void k_blind_rotate_fft<2048, 1, 4, true, 2>(const uint64_t*, int, int, const DevGate*, int,
+                                                                         const double2*, const double2*, const double2*,
+                                                                         const uint16_t*, uint64_t*, int);
+#endif
+
 // Dual shape (round 4 experiment, k = 1, FR_FFT_DUAL=1): one bootstrap per workgroup on
 // M / E = 256 lanes (4 waves), each lane holding the same slots of BOTH polynomials
 // (x[P][E]: the pair shape's B dimension carries the polynomial), two workgroups per CU.
@@ -1387,6 +1398,7 @@ k_blind_rotate_fft_dual(const uint64_t* __restrict__ ks, int ks_stride, int n, c
     }
 }
 
+#ifndef FR_BR_PAIR_TU
 // ================================================================== host side
 // compiled (k, N) points: the reference's PARAM_MESSAGE_2_CARRY_2 (k = 1, N = 2048) and
 // BASELINE's "N = 1024" set (k = 2, N = 1024, the same 2048-bit flattened key)
@@ -1541,5 +1553,7 @@ void Device::free_fft() {
     d_ftw_ = d_fqt_ = nullptr;
     d_fleaf_ = nullptr;
 }
+
+#endif  // !FR_BR_PAIR_TU
 
 }  // namespace fr

@@ -74,10 +74,12 @@ def main():
     ring = "fft" if any("blind_rotate_fft" in e.get("kernel", "") for e in launches) else "rns"
     valu = sum(e.get("valu_insts") or 0 for e in match)
     cu_clk = sum(min(e["workgroups"], 256) * e.get("grbm_gui_active_per_xcd", 0) for e in match)
-    src = os.path.join(REPO, "fhe-regex_amd", "csrc", "fft_br.hip")
+    h = hashlib.sha256()  # as bench.kernel_source_sha
+    for rel in ("csrc/fft_br.hip", "csrc/fft_br_pair.hip", "Makefile"):
+        h.update(open(os.path.join(REPO, "fhe-regex_amd", rel), "rb").read())
     res = {"hbm_bytes_per_launch": per_launch, "ring": ring, "k": int(sys.argv[3]) if len(sys.argv) > 3 else 1,
            "valu_per_cu_clk": valu / cu_clk if valu and cu_clk else None,
-           "kernel_sha": hashlib.sha256(open(src, "rb").read()).hexdigest()[:16],
+           "kernel_sha": h.hexdigest()[:16],
            "note": "FETCH_SIZE x2 (gfx950) + WRITE_SIZE, blind-rotation launches of the match, averaged per "
                    "launch; valu_per_cu_clk = sum SQ_INSTS_VALU / sum min(workgroups, 256) GRBM_GUI_ACTIVE/8",
            "launches": launches}
