@@ -15,7 +15,8 @@ from bench import make_content  # noqa: E402
 rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 9
 with open(os.path.join(REPO, "tests", "golden", "client_key"), "rb") as f:
     blob = f.read()
-ctx = F.Context(0)
+k, N = (2, 1024) if os.environ.get("FR_PARAMS") == "k2n1024" else (1, 2048)  # as lat_probe.py
+ctx = F.Context(0, params=F.default_params(k=k, N=N))
 ctx.load_client_key(blob)
 ctx.gen_server_key(42)
 hs = ctx.upload_radix(ctx.encrypt_str(make_content("printable", 256).decode(), seed=7))
